@@ -1,0 +1,161 @@
+/*
+ * nmpc_amd.h -- C-ABI of the MI355X-native batched NMPC solve step.
+ *
+ * Drop-in boundary for the per-timestep NLP of devsonni/MPC-Implementation
+ * (Python/NMPC_TT.py).  The reference builds the NLP symbolically and solves
+ * one scenario per call:
+ *
+ *   solver = ca.nlpsol('solver', 'ipopt', nlp_prob, opts)      Python/NMPC_TT.py:267
+ *   sol = solver(x0=, lbx=, ubx=, lbg=, ubg=, p=)              Python/NMPC_TT.py:358-365
+ *   u = ca.reshape(sol['x'], n_controls, N)                    Python/NMPC_TT.py:367
+ *   ff_value = ff(u, args['p'])                                Python/NMPC_TT.py:368
+ *
+ * This library replaces that pair with a handle created from a structured
+ * problem description (nmpc_create <- nlpsol) and a batched call
+ * (nmpc_solve_batch <- solver(...)), B independent scenarios per call, all
+ * solved on one MI355X by hand-written HIP kernels (one wavefront per
+ * scenario).  Plain pointers and sizes only.
+ *
+ * Layouts (match CasADi's DM column vectors / Function.map horzcat):
+ *   x0, lbx, ubx, x_out, lam_x_out : nw x B column-major, nw = 6*N   (w = vec(U), U is 6 x N)
+ *   lbg, ubg, g_out, lam_g_out     : ng x B column-major, ng = (5+n_obs)*(N+1)
+ *   p                              : np x B column-major, p = [x0(8); xs(3); dynamic obstacle coords]
+ *   X_out                          : 8*(N+1) x B column-major  (ff(u, p), Python/NMPC_TT.py:169)
+ * A leading dimension of 0 broadcasts one column to every scenario (bounds
+ * are normally shared: Python/NMPC_TT.py:269-306).  +-inf (|b| >= 1e19)
+ * means "no bound", as ca.inf does (Python/NMPC_TT.py:280-282).
+ *
+ * Errors: functions return 0 on success and a negative NMPC_E* code on
+ * invalid arguments or a HIP failure; nmpc_last_error() gives the message.
+ * Non-convergence is NOT an error (the reference never checks it):
+ * it is reported per scenario in status[] with IPOPT's ApplicationReturnStatus
+ * codes (Ipopt::Solve_Succeeded = 0, Solved_To_Acceptable_Level = 1,
+ * Search_Direction_Becomes_Too_Small = 3, Maximum_Iterations_Exceeded = -1,
+ * Restoration_Failed = -2, Error_In_Step_Computation = -3,
+ * Invalid_Number_Detected = -13).
+ *
+ * Threading/ownership: a handle is not thread-safe (one per GPU/stream).  The
+ * caller owns every buffer; nothing is retained past a call.  The handle owns
+ * its device workspace, grown on demand.
+ */
+#ifndef NMPC_AMD_H
+#define NMPC_AMD_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define NMPC_MAX_OBS 16
+#define NMPC_MAX_N 63
+
+enum {
+  NMPC_OK = 0,
+  NMPC_E_INVALID = -1, /* bad descriptor / argument */
+  NMPC_E_HIP = -2,     /* HIP runtime failure */
+  NMPC_E_NOMEM = -3    /* device allocation failed */
+};
+
+enum { NMPC_MODEL_UAV8G = 0 /* 8 states / 6 controls, Python/NMPC_TT.py:94-151 */ };
+
+/* IPOPT options honoured by the solver (names and meaning as IPOPT's;
+ * nmpc_default_options() fills IPOPT's defaults, the reference overrides
+ * max_iter=100, acceptable_tol=1e-8, acceptable_obj_change_tol=1e-6 at
+ * Python/NMPC_TT.py:257-265). */
+typedef struct nmpc_options {
+  int32_t max_iter, acceptable_iter, max_soc, max_soft_resto_iters;
+  double tol, acceptable_tol, acceptable_obj_change_tol, acceptable_dual_inf_tol;
+  double acceptable_constr_viol_tol, acceptable_compl_inf_tol;
+  double dual_inf_tol, constr_viol_tol, compl_inf_tol;
+  double mu_init, kappa_mu, theta_mu, barrier_tol_factor, tau_min;
+  double bound_push, bound_frac, slack_bound_push, slack_bound_frac, bound_relax_factor;
+  double bound_mult_init_val, constr_mult_init_max;
+  double nlp_scaling_max_gradient, nlp_scaling_min_value, kappa_d, kappa_sigma, s_max;
+  double theta_max_fact, theta_min_fact, gamma_theta, gamma_phi, delta, s_theta, s_phi, eta_phi;
+  double alpha_red_factor, alpha_min_frac, kappa_soc, obj_max_inc;
+  double first_hessian_perturbation, min_hessian_perturbation, max_hessian_perturbation;
+  double perturb_inc_fact_first, perturb_inc_fact, perturb_dec_fact;
+  double tiny_step_tol, soft_resto_pderror_reduction_factor;
+} nmpc_options;
+
+/* Structured replacement for the symbolic nlp_prob of Python/NMPC_TT.py:247-255. */
+typedef struct nmpc_desc {
+  int32_t model;    /* NMPC_MODEL_UAV8G */
+  int32_t N;        /* horizon, 1..NMPC_MAX_N (reference: 15, Python/NMPC_TT.py:58) */
+  int32_t np;       /* length of p, >= 11 */
+  int32_t n_obs;    /* 0..NMPC_MAX_OBS obstacle rows per stage */
+  double T;         /* Euler step (Python/NMPC_TT.py:57; 0.2 in 10_obstacles.py:95) */
+  double w1, w2;    /* cost weights (Python/NMPC_TT.py:204-205) */
+  double vfov, hfov;/* FOV angles (Python/NMPC_TT.py:201-202) */
+  double obs_x[NMPC_MAX_OBS], obs_y[NMPC_MAX_OBS];
+  double obs_rsum[NMPC_MAX_OBS];      /* UAV_r + obs_r (Python/NMPC_TT.py:230-231) */
+  int32_t obs_x_pidx[NMPC_MAX_OBS];   /* -1 = constant, else index into p (dynamic obstacles) */
+  int32_t obs_y_pidx[NMPC_MAX_OBS];
+  nmpc_options opts;
+} nmpc_desc;
+
+typedef struct nmpc_handle nmpc_handle;
+
+/* Fill IPOPT's default option values. */
+void nmpc_default_options(nmpc_options* opts);
+
+/* Replaces ca.nlpsol('solver', 'ipopt', nlp_prob, opts) (Python/NMPC_TT.py:267).
+ * Binds the current HIP device. */
+int nmpc_create(const nmpc_desc* desc, nmpc_handle** out);
+int nmpc_destroy(nmpc_handle* h);
+
+/* Problem dimensions: nw = 6N, ng = (5+n_obs)(N+1), np, nX = 8(N+1). */
+int nmpc_dims(const nmpc_handle* h, int32_t* nw, int32_t* ng, int32_t* np, int32_t* nX);
+
+/* Replaces sol = solver(x0=, lbx=, ubx=, lbg=, ubg=, p=) (Python/NMPC_TT.py:358-365)
+ * for B scenarios at once.  HOST pointers; synchronous.  Output pointers other
+ * than x_out may be NULL. */
+int nmpc_solve_batch(nmpc_handle* h, int32_t B,
+                     const double* x0, int64_t ld_x0,
+                     const double* lbx, int64_t ld_lbx, const double* ubx, int64_t ld_ubx,
+                     const double* lbg, int64_t ld_lbg, const double* ubg, int64_t ld_ubg,
+                     const double* p, int64_t ld_p,
+                     double* x_out, double* f_out, double* g_out,
+                     double* lam_x_out, double* lam_g_out, double* X_out,
+                     int32_t* status, int32_t* iters);
+
+/* Same with DEVICE pointers, enqueued on `stream` (hipStream_t; NULL = default
+ * stream); returns without synchronising.  Outputs other than x_out may be NULL. */
+int nmpc_solve_batch_dev(nmpc_handle* h, int32_t B,
+                         const double* x0, int64_t ld_x0,
+                         const double* lbx, int64_t ld_lbx, const double* ubx, int64_t ld_ubx,
+                         const double* lbg, int64_t ld_lbg, const double* ubg, int64_t ld_ubg,
+                         const double* p, int64_t ld_p,
+                         double* x_out, double* f_out, double* g_out,
+                         double* lam_x_out, double* lam_g_out, double* X_out,
+                         int32_t* status, int32_t* iters, void* stream);
+
+/* Optional per-iteration trace (debugging / parity): when enabled, the next
+ * solve records NMPC_TRACE_FIELDS doubles per iteration per scenario
+ * {iter, mu, f_scaled, theta, delta_w, alpha_pr, alpha_du, ls_trials}
+ * into a device buffer readable with nmpc_read_trace (host pointer,
+ * B x (max_iter+1) x NMPC_TRACE_FIELDS, row-major). */
+#define NMPC_TRACE_FIELDS 8
+int nmpc_set_trace(nmpc_handle* h, int32_t enable);
+int nmpc_read_trace(nmpc_handle* h, int32_t B, double* host_out);
+
+/* Closed-loop shift (the caller side of the solve, Python/NMPC_TT.py:13-30),
+ * on DEVICE pointers, enqueued on `stream`: for each scenario, x0 <- x0 + T f(x0,u0),
+ * warm start u <- [u(:,2:N), u(:,N)], target xs <- xs + T [v cos, v sin, w].
+ * p (np x B, ld_p) is updated in place (x0 = p[0:8], xs = p[8:11]); w_out
+ * (nw x B) receives the shifted warm start; v_t, w_t (length B) are the target
+ * speeds (Python/NMPC_TT.py:25). */
+int nmpc_shift_dev(nmpc_handle* h, int32_t B, double* p, int64_t ld_p,
+                   const double* u_sol, double* w_out,
+                   const double* v_t, const double* w_t, void* stream);
+
+const char* nmpc_last_error(void);
+
+/* Launch geometry / workspace of the last solve, for measurement. */
+int nmpc_kernel_info(const nmpc_handle* h, int32_t* lds_bytes, int32_t* threads_per_scenario);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* NMPC_AMD_H */

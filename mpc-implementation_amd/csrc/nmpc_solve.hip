@@ -1,0 +1,1824 @@
+// nmpc_solve.hip -- MI355X (gfx950) batched NMPC solve step + C-ABI (include/nmpc_amd.h).
+//
+// Replaces, for B independent scenarios per call, the per-timestep
+//   sol = solver(x0=, lbx=, ubx=, lbg=, ubg=, p=)        Python/NMPC_TT.py:358-365
+// of the reference, whose solver is ca.nlpsol('solver','ipopt',...) on the
+// single-shooting NLP of Python/NMPC_TT.py:139-267.
+//
+// Execution model: ONE WAVEFRONT (64 lanes) PER SCENARIO, the
+// whole interior-point solve inside one kernel launch, all control flow
+// wave-uniform (every branch decision comes from a butterfly all-reduce, so
+// every lane holds the bit-identical value).  Lanes parallelise:
+//   * stages   (lane k = horizon stage k, N <= 63): rollout by per-lane
+//     in-order prefix sums, derivatives, constraint rows, adjoint suffix sums;
+//   * matrix entries (lane = 8*i + j) in the Riccati backward sweep;
+//   * rows / controls (strided) for fraction-to-boundary, barrier terms,
+//     multiplier updates and optimality-error reductions.
+// Per-scenario iterate, sensitivities and the Riccati factors live in LDS.
+//
+// Algorithm: the IPOPT restatement of oracle/nmpc_oracle.py::IpoptDense,
+// step for step (same options, same decisions), except that the Newton
+// system  (W + Sigma_x + delta I + J^T D J) dU = -rhs  of the single-shooting
+// NLP is solved with a Riccati recursion on the multiple-shooting structure
+// (X re-simulated every step, defect multipliers = adjoint), which yields the
+// identical step in exact arithmetic; inertia = all Riccati pivots positive.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+
+#include "nmpc_amd.h"
+
+namespace {
+
+constexpr int WAVE = 64;
+constexpr double BIGB = 1e19;  // IPOPT nlp_{lower,upper}_bound_inf
+constexpr int FCAP = 128;      // filter capacity (>= max_iter of the reference opts)
+constexpr int TRACE_F = NMPC_TRACE_FIELDS;
+
+// ---- status codes (IPOPT ApplicationReturnStatus) ----
+constexpr int ST_SUCCESS = 0, ST_ACCEPTABLE = 1, ST_TINY = 3, ST_MAXITER = -1,
+              ST_RESTO_FAIL = -2, ST_STEP_ERR = -3, ST_INVALID_PROBLEM = -11,
+              ST_INVALID_NUMBER = -13;
+
+struct Params {
+  int N, m, nobs, np, nw, ng, nX;
+  double T, w1, w2, hv, hh;
+  double ox[NMPC_MAX_OBS], oy[NMPC_MAX_OBS], orr[NMPC_MAX_OBS];
+  int oxp[NMPC_MAX_OBS], oyp[NMPC_MAX_OBS];
+  nmpc_options o;
+  // LDS layout, offsets in doubles
+  int U, Ut, dU, dU2, zl, zu, xl, xu, sigx, ru;
+  int X, Xt, dX, dX2;
+  int s, y, vl, vu, d, dt, ds, ds2, dc, dl, du, dms;
+  int gl, Hl, trig, st, lam;
+  int K, kf, Lc, P0, P1, pv0, pv1, PA, BtP, St;
+  int p, ob, inc, filt, red;
+  int total;
+};
+
+struct IO {
+  const double *x0, *lbx, *ubx, *lbg, *ubg, *p;
+  long long ld_x0, ld_lbx, ld_ubx, ld_lbg, ld_ubg, ld_p;
+  double *x_out, *f_out, *g_out, *lam_x, *lam_g, *X_out;
+  int *status, *iters;
+  double* trace;
+};
+
+__device__ __forceinline__ double wsum(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, WAVE);
+  return v;
+}
+__device__ __forceinline__ double wmax(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, WAVE));
+  return v;
+}
+__device__ __forceinline__ double wmin(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmin(v, __shfl_xor(v, o, WAVE));
+  return v;
+}
+__device__ __forceinline__ bool wany(bool b) { return __any((int)b) != 0; }
+__device__ __forceinline__ void sync() { __syncthreads(); }
+
+// packed index of the symmetric 6x6 local (x,y,z,x5,x6,x7) Hessian, a <= b
+__device__ __forceinline__ int hp(int a, int b) {
+  if (a > b) { int t = a; a = b; b = t; }
+  return a * 6 - (a * (a - 1)) / 2 + (b - a);
+}
+// state index -> local cost-variable index (-1 if the cost does not depend on it)
+__device__ __forceinline__ int vloc(int i) {
+  return i < 3 ? i : (i >= 5 ? i - 2 : -1);
+}
+__device__ __forceinline__ int boxidx(int i) {  // g rows 0..4: z, theta, x5, x6, x7 (NMPC_TT.py:236-240)
+  return i == 0 ? 2 : (i == 1 ? 3 : 3 + i);
+}
+
+enum SumMode { SUM_NEWTON = 0, SUM_LS = 1, SUM_SOC = 2 };
+
+struct Solver {
+  const Params* __restrict__ P;
+  double* sm;
+  int lane, b;
+  int N, m, nobs, nw, ng;
+  double T;
+  // pointers into LDS
+  double *U, *Ut, *dU, *dU2, *zl, *zu, *xl, *xu, *sigx, *ru;
+  double *X, *Xt, *dX, *dX2;
+  double *s, *y, *vl, *vu, *d, *dt, *ds, *ds2, *dc, *dl, *du, *dms;
+  double *gl, *Hl, *trig, *st, *lam;
+  double *K, *kf, *Lc, *Pa, *Pb, *pva, *pvb, *PA, *BtP, *St;
+  double *pp, *obx, *oby, *inc, *filt;
+  // uniform scalars
+  double df, mu, tau, delta;
+  int nfilt;
+  int nzx, nzs;
+
+  __device__ void bind(const Params* prm, double* smem, int lane_, int b_) {
+    P = prm; sm = smem; lane = lane_; b = b_;
+    N = prm->N; m = prm->m; nobs = prm->nobs; nw = prm->nw; ng = prm->ng; T = prm->T;
+    U = sm + prm->U; Ut = sm + prm->Ut; dU = sm + prm->dU; dU2 = sm + prm->dU2;
+    zl = sm + prm->zl; zu = sm + prm->zu; xl = sm + prm->xl; xu = sm + prm->xu;
+    sigx = sm + prm->sigx; ru = sm + prm->ru;
+    X = sm + prm->X; Xt = sm + prm->Xt; dX = sm + prm->dX; dX2 = sm + prm->dX2;
+    s = sm + prm->s; y = sm + prm->y; vl = sm + prm->vl; vu = sm + prm->vu;
+    d = sm + prm->d; dt = sm + prm->dt; ds = sm + prm->ds; ds2 = sm + prm->ds2;
+    dc = sm + prm->dc; dl = sm + prm->dl; du = sm + prm->du; dms = sm + prm->dms;
+    gl = sm + prm->gl; Hl = sm + prm->Hl; trig = sm + prm->trig; st = sm + prm->st;
+    lam = sm + prm->lam;
+    K = sm + prm->K; kf = sm + prm->kf; Lc = sm + prm->Lc;
+    Pa = sm + prm->P0; Pb = sm + prm->P1; pva = sm + prm->pv0; pvb = sm + prm->pv1;
+    PA = sm + prm->PA; BtP = sm + prm->BtP; St = sm + prm->St;
+    pp = sm + prm->p; obx = sm + prm->ob; oby = obx + NMPC_MAX_OBS; inc = sm + prm->inc;
+    filt = sm + prm->filt;
+  }
+
+  __device__ __forceinline__ bool hasl(double v) const { return v > -INFINITY; }
+  __device__ __forceinline__ bool hasu(double v) const { return v < INFINITY; }
+
+  // ------------------------------------------------------------------ rollout
+  // X[:,0] = p[0:8]; X[:,k+1] = X[:,k] + T f(X[:,k],U[:,k])   (NMPC_TT.py:160-167)
+  // Each lane k sums the increments j<k in order, i.e. bitwise the sequential
+  // recursion; the (x,y,z) increments need theta_j, psi_j, so two passes.
+  __device__ void rollout(const double* Us, double* Xd) {
+    const int k = lane;
+    if (k < N) {
+#pragma unroll
+      for (int c = 0; c < 5; ++c) inc[k * 8 + c] = T * Us[k * 6 + 1 + c];
+    }
+    sync();
+    double a[5];
+    if (k <= N) {
+#pragma unroll
+      for (int c = 0; c < 5; ++c) a[c] = pp[3 + c];
+      for (int j = 0; j < k; ++j) {
+#pragma unroll
+        for (int c = 0; c < 5; ++c) a[c] = a[c] + inc[j * 8 + c];
+      }
+      if (k < N) {
+        const double v = Us[k * 6];
+        const double ct = cos(a[0]), st_ = sin(a[0]), cp = cos(a[1]), sp = sin(a[1]);
+        inc[k * 8 + 5] = T * (v * cp * ct);
+        inc[k * 8 + 6] = T * (v * sp * ct);
+        inc[k * 8 + 7] = T * (v * st_);
+      }
+    }
+    sync();
+    if (k <= N) {
+      double c0 = pp[0], c1 = pp[1], c2 = pp[2];
+      for (int j = 0; j < k; ++j) {
+        c0 = c0 + inc[j * 8 + 5];
+        c1 = c1 + inc[j * 8 + 6];
+        c2 = c2 + inc[j * 8 + 7];
+      }
+      double* xk = Xd + k * 8;
+      xk[0] = c0; xk[1] = c1; xk[2] = c2;
+#pragma unroll
+      for (int c = 0; c < 5; ++c) xk[3 + c] = a[c];
+    }
+    sync();
+  }
+
+  // ---------------------------------------------------------- stage cost value
+  // Literal restatement of NMPC_TT.py:209-220 (same operation order as the
+  // oracle's stage_cost).
+  __device__ double stage_cost(const double* x) const {
+    const double hv = P->hv, hh = P->hh;
+    const double z = x[2];
+    const double a = (z * tan(x[6] + hv) - z * tan(x[6] - hv)) / 2;
+    const double bb = (z * tan(x[5] + hh) - z * tan(x[5] - hh)) / 2;
+    const double c7 = cos(x[7]), s7 = sin(x[7]);
+    const double a2 = a * a, b2 = bb * bb;
+    const double A = (c7 * c7) / a2 + (s7 * s7) / b2;
+    const double Bq = 2 * c7 * s7 * ((1 / a2) - (1 / b2));
+    const double C = (s7 * s7) / a2 + (c7 * c7) / b2;
+    const double XE = x[0] + a + z * tan(x[6] - hv);
+    const double YE = x[1] + bb + z * tan(x[5] - hh);
+    const double xt = pp[8], yt = pp[9];
+    const double ex = xt - XE, ey = yt - YE;
+    const double dx = x[0] - xt, dy = x[1] - yt;
+    return P->w1 * sqrt(dx * dx + dy * dy) +
+           P->w2 * ((A * (ex * ex) + Bq * ey * ex + C * (ey * ey)) - 1);
+  }
+
+  __device__ __forceinline__ double row_value(const double* x, int i) const {
+    if (i < 5) return x[boxidx(i)];
+    const int o = i - 5;
+    const double ddx = x[0] - obx[o], ddy = x[1] - oby[o];
+    return -sqrt(ddx * ddx + ddy * ddy) + P->orr[o];
+  }
+
+  // f = sum_k l_k(X) and rows dst[r] = dc[r] * g_r(X) (dc may be null -> unscaled)
+  __device__ double eval_fg(const double* Xs, double* dst, const double* scale) {
+    const int k = lane;
+    double f = 0.0;
+    if (k <= N) {
+      const double* xk = Xs + k * 8;
+      if (k < N) f = stage_cost(xk);
+      for (int i = 0; i < m; ++i) {
+        const int r = k * m + i;
+        const double g = row_value(xk, i);
+        dst[r] = scale ? scale[r] * g : g;
+      }
+    }
+    sync();
+    return wsum(f);
+  }
+
+  // --------------------------------------------- stage derivatives at X (lane=k)
+  // gl[k] = grad l_k (8), Hl[k] = hess l_k packed over (x,y,z,x5,x6,x7), trig[k].
+  // Derivation: oracle/nmpc_oracle.py::stage_cost_derivs (Q = (r1/a)^2+(r2/b)^2).
+  __device__ void derivs(const double* Xs, const double* Us) {
+    const int k = lane;
+    if (k <= N) {
+      const double* xk = Xs + k * 8;
+      const double th = xk[3], ps = xk[4];
+      double* tg = trig + k * 8;
+      tg[0] = cos(th); tg[1] = sin(th); tg[2] = cos(ps); tg[3] = sin(ps);
+      tg[4] = (k < N) ? Us[k * 6] : 0.0;
+      double* g8 = gl + k * 8;
+      double* H = Hl + k * 21;
+      if (k == N) {
+        for (int i = 0; i < 8; ++i) g8[i] = 0.0;
+        for (int i = 0; i < 21; ++i) H[i] = 0.0;
+      } else {
+        const double hv = P->hv, hh = P->hh;
+        const double x = xk[0], yy = xk[1], z = xk[2], x5 = xk[5], x6 = xk[6], x7 = xk[7];
+        const double xt = pp[8], yt = pp[9];
+        const double t6p = tan(x6 + hv), t6m = tan(x6 - hv);
+        const double t5p = tan(x5 + hh), t5m = tan(x5 - hh);
+        const double al6 = (t6p - t6m) / 2, be6 = (t6p + t6m) / 2;
+        const double al5 = (t5p - t5m) / 2, be5 = (t5p + t5m) / 2;
+        const double al6d = (t6p * t6p - t6m * t6m) / 2, be6d = (2 + t6p * t6p + t6m * t6m) / 2;
+        const double al5d = (t5p * t5p - t5m * t5m) / 2, be5d = (2 + t5p * t5p + t5m * t5m) / 2;
+        const double s6p = t6p * (1 + t6p * t6p), s6m = t6m * (1 + t6m * t6m);
+        const double s5p = t5p * (1 + t5p * t5p), s5m = t5m * (1 + t5m * t5m);
+        const double al6dd = s6p - s6m, be6dd = s6p + s6m;
+        const double al5dd = s5p - s5m, be5dd = s5p + s5m;
+        const double ex = xt - x - z * be6;
+        const double ey = yt - yy - z * be5;
+        double gex[6] = {-1.0, 0.0, -be6, 0.0, -z * be6d, 0.0};
+        double gey[6] = {0.0, -1.0, -be5, -z * be5d, 0.0, 0.0};
+        const double a = z * al6, bb = z * al5;
+        double ga[6] = {0.0, 0.0, al6, 0.0, z * al6d, 0.0};
+        double gb[6] = {0.0, 0.0, al5, z * al5d, 0.0, 0.0};
+        const double c = cos(x7), sn = sin(x7);
+        const double r1 = c * ex + sn * ey;
+        const double r2 = sn * ex - c * ey;
+        double u1[6], u2[6], gr1[6], gr2[6], ge1[6], ge2[6];
+        const double e1 = r1 / a, e2 = r2 / bb;
+#pragma unroll
+        for (int q = 0; q < 6; ++q) {
+          u1[q] = -sn * gex[q] + c * gey[q];
+          u2[q] = c * gex[q] + sn * gey[q];
+          gr1[q] = c * gex[q] + sn * gey[q] - (q == 5 ? r2 : 0.0);
+          gr2[q] = sn * gex[q] - c * gey[q] + (q == 5 ? r1 : 0.0);
+          ge1[q] = (gr1[q] - e1 * ga[q]) / a;
+          ge2[q] = (gr2[q] - e2 * gb[q]) / bb;
+        }
+        const double ddx = x - xt, ddy = yy - yt;
+        const double dd = sqrt(ddx * ddx + ddy * ddy);
+        const double d3 = dd * dd * dd;
+        const double w1 = P->w1, w2 = P->w2;
+        // gradient
+        double g6[6];
+#pragma unroll
+        for (int q = 0; q < 6; ++q) g6[q] = w2 * (2 * (e1 * ge1[q] + e2 * ge2[q]));
+        g6[0] += w1 * (ddx / dd);
+        g6[1] += w1 * (ddy / dd);
+        g8[0] = g6[0]; g8[1] = g6[1]; g8[2] = g6[2]; g8[3] = 0.0; g8[4] = 0.0;
+        g8[5] = g6[3]; g8[6] = g6[4]; g8[7] = g6[5];
+        // Hessian, 21 packed entries
+#pragma unroll
+        for (int qa = 0; qa < 6; ++qa) {
+#pragma unroll
+          for (int qb = qa; qb < 6; ++qb) {
+            // sparse second derivatives of ex, ey, a, b
+            double Hex = 0.0, Hey = 0.0, Ha = 0.0, Hb = 0.0;
+            if ((qa == 2 && qb == 4)) { Hex = -be6d; Ha = al6d; }
+            if (qa == 4 && qb == 4) { Hex = -z * be6dd; Ha = z * al6dd; }
+            if ((qa == 2 && qb == 3)) { Hey = -be5d; Hb = al5d; }
+            if (qa == 3 && qb == 3) { Hey = -z * be5dd; Hb = z * al5dd; }
+            const double e7a = (qa == 5) ? 1.0 : 0.0, e7b = (qb == 5) ? 1.0 : 0.0;
+            const double Hr1 = c * Hex + sn * Hey + e7a * u1[qb] + u1[qa] * e7b - r1 * e7a * e7b;
+            const double Hr2 = sn * Hex - c * Hey + e7a * u2[qb] + u2[qa] * e7b - r2 * e7a * e7b;
+            const double He1 = (Hr1 - ge1[qa] * ga[qb] - ga[qa] * ge1[qb] - e1 * Ha) / a;
+            const double He2 = (Hr2 - ge2[qa] * gb[qb] - gb[qa] * ge2[qb] - e2 * Hb) / bb;
+            double h = w2 * (2 * (ge1[qa] * ge1[qb] + ge2[qa] * ge2[qb] + e1 * He1 + e2 * He2));
+            if (qa == 0 && qb == 0) h += w1 * (ddy * ddy / d3);
+            if (qa == 0 && qb == 1) h += w1 * (-ddx * ddy / d3);
+            if (qa == 1 && qb == 1) h += w1 * (ddx * ddx / d3);
+            H[hp(qa, qb)] = h;
+          }
+        }
+      }
+    }
+    sync();
+  }
+
+  // E entries of A_k = I + E_k and first column b0 of B_k (oracle dyn_jac)
+  __device__ __forceinline__ void stage_AB(int k, double& E03, double& E04, double& E13,
+                                           double& E14, double& E23, double& b00, double& b10,
+                                           double& b20) const {
+    const double* tg = trig + k * 8;
+    const double ct = tg[0], stt = tg[1], cp = tg[2], sp = tg[3], v = tg[4];
+    E03 = -T * v * cp * stt; E04 = -T * v * sp * ct;
+    E13 = -T * v * sp * stt; E14 = T * v * cp * ct;
+    E23 = T * v * ct;
+    b00 = T * cp * ct; b10 = T * sp * ct; b20 = T * stt;
+  }
+
+  // --------------------------------------------- adjoint lam_k (lane = k)
+  // lam_N = G_N^T y_N; lam_k = ofac*gl_k + G_k^T y_k + A_k^T lam_{k+1}
+  // (oracle SSEval.hessian).  yy may be null (objective only).
+  __device__ void adjoint(double ofac, const double* yy) {
+    const int k = lane;
+    double* wv = inc;  // scratch 8*(N+1)
+    if (k <= N) {
+      double w[8];
+      const double* xk = X + k * 8;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) w[i] = ofac * gl[k * 8 + i];
+      if (yy) {
+        for (int i = 0; i < 5; ++i) {
+          const int r = k * m + i;
+          w[boxidx(i)] += dc[r] * yy[r];
+        }
+        for (int o = 0; o < nobs; ++o) {
+          const int r = k * m + 5 + o;
+          const double ddx = xk[0] - obx[o], ddy = xk[1] - oby[o];
+          const double dd = sqrt(ddx * ddx + ddy * ddy);
+          const double cy = dc[r] * yy[r];
+          w[0] += cy * (-(ddx / dd));
+          w[1] += cy * (-(ddy / dd));
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i) wv[k * 8 + i] = w[i];
+    }
+    sync();
+    if (k <= N) {
+      const int cs[6] = {0, 1, 2, 5, 6, 7};
+#pragma unroll
+      for (int q = 0; q < 6; ++q) {
+        const int c = cs[q];
+        double acc = wv[N * 8 + c];
+        for (int j = N - 1; j >= k; --j) acc = wv[j * 8 + c] + acc;
+        lam[k * 8 + c] = acc;
+      }
+    }
+    sync();
+    if (k <= N) {
+      double a3 = wv[N * 8 + 3], a4 = wv[N * 8 + 4];
+      for (int j = N - 1; j >= k; --j) {
+        double E03, E04, E13, E14, E23, b00, b10, b20;
+        stage_AB(j, E03, E04, E13, E14, E23, b00, b10, b20);
+        const double* ln = lam + (j + 1) * 8;
+        a3 = wv[j * 8 + 3] + (((E03 * ln[0] + E13 * ln[1]) + E23 * ln[2]) + a3);
+        a4 = wv[j * 8 + 4] + ((E04 * ln[0] + E14 * ln[1]) + a4);
+      }
+      lam[k * 8 + 3] = a3;
+      lam[k * 8 + 4] = a4;
+    }
+    sync();
+  }
+
+  // dL/du_k[c] = (B_k^T lam_{k+1})[c]
+  __device__ __forceinline__ double grad_u(int i) const {
+    const int k = i / 6, c = i - 6 * (i / 6);
+    const double* ln = lam + (k + 1) * 8;
+    if (c == 0) {
+      const double* tg = trig + k * 8;
+      const double ct = tg[0], stt = tg[1], cp = tg[2], sp = tg[3];
+      return (T * cp * ct) * ln[0] + (T * sp * ct) * ln[1] + (T * stt) * ln[2];
+    }
+    return T * ln[2 + c];
+  }
+
+  // ------------------------------------------------ slacks / barrier helpers
+  __device__ __forceinline__ double sl_x(int i, const double* u) const { return u[i] - xl[i]; }
+  __device__ __forceinline__ double su_x(int i, const double* u) const { return xu[i] - u[i]; }
+
+  // barrier objective phi (oracle barrier_obj) at (u, s + a*ds) [sv == null -> s]
+  __device__ double barrier_obj(double f, const double* u, const double* sb, const double* dsv,
+                                double a) const {
+    double logs = 0.0, damp = 0.0;
+    for (int i = lane; i < nw; i += WAVE) {
+      const bool lo = hasl(xl[i]), hi = hasu(xu[i]);
+      if (lo) logs += log(u[i] - xl[i]);
+      if (hi) logs += log(xu[i] - u[i]);
+      if (lo && !hi) damp += u[i] - xl[i];
+      if (hi && !lo) damp += xu[i] - u[i];
+    }
+    for (int r = lane; r < ng; r += WAVE) {
+      const double sv = dsv ? sb[r] + a * dsv[r] : sb[r];
+      const bool lo = hasl(dl[r]), hi = hasu(du[r]);
+      if (lo) logs += log(sv - dl[r]);
+      if (hi) logs += log(du[r] - sv);
+      if (lo && !hi) damp += sv - dl[r];
+      if (hi && !lo) damp += du[r] - sv;
+    }
+    logs = wsum(logs);
+    damp = wsum(damp);
+    return f - mu * logs + P->o.kappa_d * mu * damp;
+  }
+
+  // -------------------------------------------- Riccati: per-stage summaries
+  // st[k] = {Qxy(3), Qbox(5), qxy(2), qbox(5)}: contributions of the stage-k
+  // rows to the stage Hessian / gradient.  Modes:
+  //  NEWTON: Q += Gt^T D Gt + sum_obs y dc Hg ; q += Gt^T (y + D rd + rs)
+  //  SOC:    q only, with rd := dms
+  //  LS:     Q += Gt^T Gt ; q += -Gt^T (vu - vl)           (least-squares y init)
+  __device__ void summaries(int mode) {
+    const int k = lane;
+    if (k <= N) {
+      const double* xk = X + k * 8;
+      double Qxy0 = 0, Qxy1 = 0, Qxy2 = 0, qx = 0, qy = 0;
+      double Qb[5], qb[5];
+      const double kd = P->o.kappa_d;
+      for (int i = 0; i < m; ++i) {
+        const int r = k * m + i;
+        double A, Bw, C = 0.0;
+        if (mode == SUM_LS) {
+          A = 1.0;
+          Bw = -(vu[r] - vl[r]);
+        } else {
+          const bool lo = hasl(dl[r]), hi = hasu(du[r]);
+          const double Sl = lo ? s[r] - dl[r] : 1.0, Su = hi ? du[r] - s[r] : 1.0;
+          const double sig = (lo ? vl[r] / Sl : 0.0) + (hi ? vu[r] / Su : 0.0);
+          const double D = sig + delta;
+          const double rs = -y[r] - (lo ? mu / Sl : 0.0) + (hi ? mu / Su : 0.0) +
+                            kd * mu * ((lo && !hi ? 1.0 : 0.0) - (hi && !lo ? 1.0 : 0.0));
+          const double rd = (mode == SUM_SOC) ? dms[r] : d[r] - s[r];
+          A = D;
+          Bw = y[r] + D * rd + rs;
+          C = y[r] * dc[r];
+        }
+        if (i < 5) {
+          Qb[i] = dc[r] * dc[r] * A;
+          qb[i] = dc[r] * Bw;
+        } else {
+          const int o = i - 5;
+          const double ddx = xk[0] - obx[o], ddy = xk[1] - oby[o];
+          const double dd = sqrt(ddx * ddx + ddy * ddy);
+          const double gx = -(ddx / dd), gy = -(ddy / dd);
+          const double d3 = dd * dd * dd;
+          const double w = dc[r] * dc[r] * A;
+          Qxy0 += w * gx * gx + C * (-ddy * ddy / d3);
+          Qxy1 += w * gx * gy + C * (ddx * ddy / d3);
+          Qxy2 += w * gy * gy + C * (-ddx * ddx / d3);
+          qx += dc[r] * Bw * gx;
+          qy += dc[r] * Bw * gy;
+        }
+      }
+      double* o16 = st + k * 16;
+      o16[0] = Qxy0; o16[1] = Qxy1; o16[2] = Qxy2;
+#pragma unroll
+      for (int i = 0; i < 5; ++i) { o16[3 + i] = Qb[i]; o16[10 + i] = qb[i]; }
+      o16[8] = qx; o16[9] = qy;
+    }
+    sync();
+  }
+
+  // stage Hessian entry Q_k[i][j] (hfac*Hl + rows + dynamics with lam_{k+1})
+  __device__ __forceinline__ double Qentry(int k, int i, int j, double hfac, bool dyn) const {
+    double q = 0.0;
+    const int vi = vloc(i), vj = vloc(j);
+    if (vi >= 0 && vj >= 0) q += hfac * Hl[k * 21 + hp(vi, vj)];
+    const double* o16 = st + k * 16;
+    if (i < 2 && j < 2) q += o16[i + j];  // Qxy0 (0,0), Qxy1 (0,1)/(1,0), Qxy2 (1,1)
+    if (i == j) {
+      if (i == 2) q += o16[3];
+      else if (i == 3) q += o16[4];
+      else if (i >= 5) q += o16[i + 0];  // 5->o16[5], 6->o16[6], 7->o16[7]
+    }
+    if (dyn && k < N && (i == 3 || i == 4) && (j == 3 || j == 4)) {
+      const double* tg = trig + k * 8;
+      const double ct = tg[0], stt = tg[1], cp = tg[2], sp = tg[3], v = tg[4];
+      const double* ln = lam + (k + 1) * 8;
+      const double l0 = ln[0], l1 = ln[1], l2 = ln[2];
+      if (i == 3 && j == 3) q += T * (-l0 * v * cp * ct - l1 * v * sp * ct - l2 * v * stt);
+      else if (i == 4 && j == 4) q += T * (-l0 * v * cp * ct - l1 * v * sp * ct);
+      else q += T * (l0 * v * sp * stt - l1 * v * cp * stt);
+    }
+    return q;
+  }
+  __device__ __forceinline__ double qentry(int k, int i, double gfac) const {
+    double q = gfac * gl[k * 8 + i];
+    const double* o16 = st + k * 16;
+    if (i == 0) q += o16[8];
+    else if (i == 1) q += o16[9];
+    else if (i == 2) q += o16[10];
+    else if (i == 3) q += o16[11];
+    else if (i >= 5) q += o16[7 + i];  // 5->12, 6->13, 7->14
+    return q;
+  }
+  // S_k[0][3], S_k[0][4] (dynamics cross terms, oracle dyn_hess Hxu)
+  __device__ __forceinline__ void Sdyn(int k, double& s03, double& s04) const {
+    const double* tg = trig + k * 8;
+    const double ct = tg[0], stt = tg[1], cp = tg[2], sp = tg[3];
+    const double* ln = lam + (k + 1) * 8;
+    const double l0 = ln[0], l1 = ln[1], l2 = ln[2];
+    s03 = T * (-l0 * cp * stt - l1 * sp * stt + l2 * ct);
+    s04 = T * (-l0 * sp * ct + l1 * cp * ct);
+  }
+
+  // ----------------------------------------- Riccati factorisation + solve
+  // Backward sweep over stages with lane (i,j) owning entry (i,j) of the 8x8
+  // cost-to-go matrix.  Returns false if a pivot of some R~_k is not positive
+  // (wrong inertia).  Stores K_k, k_k, chol(R~_k) for the forward sweep / SOC.
+  //   hfac, gfac: factors on the stage cost Hessian / gradient; dyn: add the
+  //   dynamics second derivatives; Rd: diag of R (null -> 1).
+  __device__ bool riccati(double hfac, double gfac, bool dyn, const double* Rd, const double* rv) {
+    const int i = lane >> 3, j = lane & 7;
+    double* Pc = Pa;
+    double* Pn = Pb;
+    double* pc = pva;
+    double* pn = pvb;
+    Pc[lane] = Qentry(N, i, j, hfac, dyn);
+    if (lane < 8) pc[lane] = qentry(N, lane, gfac);
+    sync();
+    bool ok = true;
+    for (int k = N - 1; k >= 0; --k) {
+      double E03, E04, E13, E14, E23, b00, b10, b20;
+      stage_AB(k, E03, E04, E13, E14, E23, b00, b10, b20);
+      // (A) PA = P A ; BtP = B^T P
+      {
+        const double* Pi = Pc + i * 8;
+        double v = Pi[j];
+        if (j == 3) v = v + ((Pi[0] * E03 + Pi[1] * E13) + Pi[2] * E23);
+        else if (j == 4) v = v + (Pi[0] * E04 + Pi[1] * E14);
+        PA[lane] = v;
+        if (lane < 48) {
+          const int r = i, jj = j;
+          BtP[lane] = (r == 0) ? ((b00 * Pc[jj] + b10 * Pc[8 + jj]) + b20 * Pc[16 + jj])
+                               : T * Pc[(2 + r) * 8 + jj];
+        }
+      }
+      sync();
+      // (B) APA = A^T P A (register) ; St = S + B^T P A
+      double APA;
+      {
+        double v = PA[lane];
+        if (i == 3) v = v + ((E03 * PA[j] + E13 * PA[8 + j]) + E23 * PA[16 + j]);
+        else if (i == 4) v = v + (E04 * PA[j] + E14 * PA[8 + j]);
+        APA = v;
+        if (lane < 48) {
+          const int r = i, jj = j;
+          double sv = (r == 0) ? ((b00 * PA[jj] + b10 * PA[8 + jj]) + b20 * PA[16 + jj])
+                               : T * PA[(2 + r) * 8 + jj];
+          if (dyn && r == 0 && (jj == 3 || jj == 4)) {
+            double s03, s04;
+            Sdyn(k, s03, s04);
+            sv += (jj == 3) ? s03 : s04;
+          }
+          St[lane] = sv;
+        }
+      }
+      sync();
+      // (C) every lane: R~ = R + B^T P B, Cholesky, r~ = r + B^T p
+      double Lm[21], idg[6], rt[6];
+      {
+        double R[21];
+#pragma unroll
+        for (int r = 0; r < 6; ++r) {
+#pragma unroll
+          for (int c = 0; c <= r; ++c) {
+            double v = (c == 0) ? ((BtP[r * 8 + 0] * b00 + BtP[r * 8 + 1] * b10) + BtP[r * 8 + 2] * b20)
+                                : T * BtP[r * 8 + 2 + c];
+            if (r == c) v += (Rd ? Rd[k * 6 + r] : 1.0) + delta;
+            R[r * (r + 1) / 2 + c] = v;
+          }
+        }
+#pragma unroll
+        for (int c = 0; c < 6; ++c) {
+          double dg = R[c * (c + 1) / 2 + c];
+#pragma unroll
+          for (int t = 0; t < c; ++t) dg -= Lm[c * (c + 1) / 2 + t] * Lm[c * (c + 1) / 2 + t];
+          if (!(dg > 0.0)) ok = false;
+          const double l = sqrt(dg);
+          Lm[c * (c + 1) / 2 + c] = l;
+          idg[c] = 1.0 / l;
+#pragma unroll
+          for (int r = c + 1; r < 6; ++r) {
+            double v = R[r * (r + 1) / 2 + c];
+#pragma unroll
+            for (int t = 0; t < c; ++t) v -= Lm[r * (r + 1) / 2 + t] * Lm[c * (c + 1) / 2 + t];
+            Lm[r * (r + 1) / 2 + c] = v * idg[c];
+          }
+        }
+        // r~ = r_k + B^T p_{k+1}
+        rt[0] = rv[k * 6 + 0] + ((b00 * pc[0] + b10 * pc[1]) + b20 * pc[2]);
+#pragma unroll
+        for (int r = 1; r < 6; ++r) rt[r] = rv[k * 6 + r] + T * pc[2 + r];
+      }
+      ok = !wany(!ok);  // every lane computed the same pivots; make it explicit
+      if (!ok) break;
+      // (D) K = -R~^{-1} St (lanes 0..7 one column each), kf = -R~^{-1} r~
+      {
+        if (lane < 9) {
+          double v[6];
+#pragma unroll
+          for (int r = 0; r < 6; ++r) v[r] = (lane < 8) ? St[r * 8 + lane] : rt[r];
+          // forward L z = v
+#pragma unroll
+          for (int r = 0; r < 6; ++r) {
+            double a = v[r];
+#pragma unroll
+            for (int t = 0; t < r; ++t) a -= Lm[r * (r + 1) / 2 + t] * v[t];
+            v[r] = a * idg[r];
+          }
+          // backward L^T x = z
+#pragma unroll
+          for (int r = 5; r >= 0; --r) {
+            double a = v[r];
+#pragma unroll
+            for (int t = r + 1; t < 6; ++t) a -= Lm[t * (t + 1) / 2 + r] * v[t];
+            v[r] = a * idg[r];
+          }
+          if (lane < 8) {
+#pragma unroll
+            for (int r = 0; r < 6; ++r) K[k * 48 + r * 8 + lane] = -v[r];
+          } else {
+#pragma unroll
+            for (int r = 0; r < 6; ++r) kf[k * 6 + r] = -v[r];
+          }
+        }
+        if (lane == 9) {
+          double* lc = Lc + k * 28;
+#pragma unroll
+          for (int t = 0; t < 21; ++t) lc[t] = Lm[t];
+#pragma unroll
+          for (int t = 0; t < 6; ++t) lc[21 + t] = idg[t];
+        }
+      }
+      sync();
+      // (E) P_k = Q_k + A^T P A + St^T K ; p_k = q_k + A^T p + K^T r~
+      {
+        double sk = 0.0;
+#pragma unroll
+        for (int r = 0; r < 6; ++r) sk += St[r * 8 + i] * K[k * 48 + r * 8 + j];
+        Pn[lane] = (Qentry(k, i, j, hfac, dyn) + APA) + sk;
+        if (lane < 8) {
+          double atp = pc[lane];
+          if (lane == 3) atp = atp + ((E03 * pc[0] + E13 * pc[1]) + E23 * pc[2]);
+          else if (lane == 4) atp = atp + (E04 * pc[0] + E14 * pc[1]);
+          double kr = 0.0;
+#pragma unroll
+          for (int r = 0; r < 6; ++r) kr += K[k * 48 + r * 8 + lane] * rt[r];
+          pn[lane] = (qentry(k, lane, gfac) + atp) + kr;
+        }
+      }
+      sync();
+      double* t1 = Pc; Pc = Pn; Pn = t1;
+      double* t2 = pc; pc = pn; pn = t2;
+    }
+    return ok;
+  }
+
+  // gradient-only re-solve with the stored factors (second-order correction)
+  __device__ void resolve(double gfac, const double* rv) {
+    // every lane runs the vector recursion redundantly (no LDS exchange)
+    double p8[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) p8[i] = qentry(N, i, gfac);
+    for (int k = N - 1; k >= 0; --k) {
+      double E03, E04, E13, E14, E23, b00, b10, b20;
+      stage_AB(k, E03, E04, E13, E14, E23, b00, b10, b20);
+      const double* lc = Lc + k * 28;
+      double rt[6], v[6];
+      rt[0] = rv[k * 6 + 0] + ((b00 * p8[0] + b10 * p8[1]) + b20 * p8[2]);
+#pragma unroll
+      for (int r = 1; r < 6; ++r) rt[r] = rv[k * 6 + r] + T * p8[2 + r];
+#pragma unroll
+      for (int r = 0; r < 6; ++r) {
+        double a = rt[r];
+#pragma unroll
+        for (int t = 0; t < r; ++t) a -= lc[r * (r + 1) / 2 + t] * v[t];
+        v[r] = a * lc[21 + r];
+      }
+#pragma unroll
+      for (int r = 5; r >= 0; --r) {
+        double a = v[r];
+#pragma unroll
+        for (int t = r + 1; t < 6; ++t) a -= lc[t * (t + 1) / 2 + r] * v[t];
+        v[r] = a * lc[21 + r];
+      }
+      if (lane == 0) {
+#pragma unroll
+        for (int r = 0; r < 6; ++r) kf[k * 6 + r] = -v[r];
+      }
+      double pn[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        double atp = p8[i];
+        if (i == 3) atp = atp + ((E03 * p8[0] + E13 * p8[1]) + E23 * p8[2]);
+        else if (i == 4) atp = atp + (E04 * p8[0] + E14 * p8[1]);
+        double kr = 0.0;
+#pragma unroll
+        for (int r = 0; r < 6; ++r) kr += K[k * 48 + r * 8 + i] * rt[r];
+        pn[i] = (qentry(k, i, gfac) + atp) + kr;
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i) p8[i] = pn[i];
+    }
+    sync();
+  }
+
+  // forward sweep: du_k = K_k dx_k + k_k ; dx_{k+1} = A_k dx_k + B_k du_k
+  // (redundant in every lane, broadcast LDS reads; lane 0 stores)
+  __device__ void forward(double* dUo, double* dXo) {
+    double dx[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) dx[i] = 0.0;
+    if (lane < 8) dXo[lane] = 0.0;
+    for (int k = 0; k < N; ++k) {
+      double E03, E04, E13, E14, E23, b00, b10, b20;
+      stage_AB(k, E03, E04, E13, E14, E23, b00, b10, b20);
+      double du_[6];
+#pragma unroll
+      for (int r = 0; r < 6; ++r) {
+        double a = kf[k * 6 + r];
+#pragma unroll
+        for (int c = 0; c < 8; ++c) a += K[k * 48 + r * 8 + c] * dx[c];
+        du_[r] = a;
+      }
+      double xn[8];
+      xn[0] = dx[0] + (E03 * dx[3] + E04 * dx[4]) + b00 * du_[0];
+      xn[1] = dx[1] + (E13 * dx[3] + E14 * dx[4]) + b10 * du_[0];
+      xn[2] = dx[2] + E23 * dx[3] + b20 * du_[0];
+#pragma unroll
+      for (int c = 0; c < 5; ++c) xn[3 + c] = dx[3 + c] + T * du_[1 + c];
+      if (lane == 0) {
+#pragma unroll
+        for (int r = 0; r < 6; ++r) dUo[k * 6 + r] = du_[r];
+#pragma unroll
+        for (int c = 0; c < 8; ++c) dXo[(k + 1) * 8 + c] = xn[c];
+      }
+#pragma unroll
+      for (int c = 0; c < 8; ++c) dx[c] = xn[c];
+    }
+    sync();
+  }
+
+  // ds_r = Gt_r dX_k + rd_r (J dU = G Z dU = G dX)
+  __device__ void row_step(const double* dXs, const double* rdsrc, bool rd_is_dms, double* dso) {
+    for (int r = lane; r < ng; r += WAVE) {
+      const int k = r / m, i = r - k * m;
+      const double* xk = X + k * 8;
+      const double* dxk = dXs + k * 8;
+      double jd;
+      if (i < 5) {
+        jd = dc[r] * dxk[boxidx(i)];
+      } else {
+        const int o = i - 5;
+        const double ddx = xk[0] - obx[o], ddy = xk[1] - oby[o];
+        const double dd = sqrt(ddx * ddx + ddy * ddy);
+        jd = dc[r] * ((-(ddx / dd)) * dxk[0] + (-(ddy / dd)) * dxk[1]);
+      }
+      const double rd = rd_is_dms ? rdsrc[r] : d[r] - s[r];
+      dso[r] = jd + rd;
+    }
+    sync();
+  }
+
+  // primal fraction to the boundary (oracle frac_to_bound)
+  __device__ double frac_to_bound(double tau_, const double* dUs, const double* dss) const {
+    double a = 1.0;
+    for (int i = lane; i < nw; i += WAVE) {
+      const double dx = dUs[i];
+      if (hasl(xl[i]) && dx < 0) a = fmin(a, (-tau_ * (U[i] - xl[i])) / dx);
+      if (hasu(xu[i]) && -dx < 0) a = fmin(a, (-tau_ * (xu[i] - U[i])) / (-dx));
+    }
+    for (int r = lane; r < ng; r += WAVE) {
+      const double dd = dss[r];
+      if (hasl(dl[r]) && dd < 0) a = fmin(a, (-tau_ * (s[r] - dl[r])) / dd);
+      if (hasu(du[r]) && -dd < 0) a = fmin(a, (-tau_ * (du[r] - s[r])) / (-dd));
+    }
+    return wmin(a);
+  }
+
+  // dual step components (oracle solve_dir) -- current slacks
+  __device__ __forceinline__ void dz_x(int i, double dx, double& dzl, double& dzu) const {
+    dzl = 0.0; dzu = 0.0;
+    if (hasl(xl[i])) { const double S = U[i] - xl[i]; dzl = mu / S - zl[i] - zl[i] / S * dx; }
+    if (hasu(xu[i])) { const double S = xu[i] - U[i]; dzu = mu / S - zu[i] + zu[i] / S * dx; }
+  }
+  __device__ __forceinline__ void dv_s(int r, double dsv, double& dvl, double& dvu) const {
+    dvl = 0.0; dvu = 0.0;
+    if (hasl(dl[r])) { const double S = s[r] - dl[r]; dvl = mu / S - vl[r] - vl[r] / S * dsv; }
+    if (hasu(du[r])) { const double S = du[r] - s[r]; dvu = mu / S - vu[r] + vu[r] / S * dsv; }
+  }
+  __device__ double dual_frac_to_bound(double tau_, const double* dUs, const double* dss) const {
+    double a = 1.0;
+    for (int i = lane; i < nw; i += WAVE) {
+      double a1, a2;
+      dz_x(i, dUs[i], a1, a2);
+      if (hasl(xl[i]) && a1 < 0) a = fmin(a, (-tau_ * zl[i]) / a1);
+      if (hasu(xu[i]) && a2 < 0) a = fmin(a, (-tau_ * zu[i]) / a2);
+    }
+    for (int r = lane; r < ng; r += WAVE) {
+      double a1, a2;
+      dv_s(r, dss[r], a1, a2);
+      if (hasl(dl[r]) && a1 < 0) a = fmin(a, (-tau_ * vl[r]) / a1);
+      if (hasu(du[r]) && a2 < 0) a = fmin(a, (-tau_ * vu[r]) / a2);
+    }
+    return wmin(a);
+  }
+
+  // rs_r (oracle rs) and D_r
+  __device__ __forceinline__ void row_rs(int r, double& D, double& rs) const {
+    const bool lo = hasl(dl[r]), hi = hasu(du[r]);
+    const double Sl = lo ? s[r] - dl[r] : 1.0, Su = hi ? du[r] - s[r] : 1.0;
+    D = (lo ? vl[r] / Sl : 0.0) + (hi ? vu[r] / Su : 0.0) + delta;
+    rs = -y[r] - (lo ? mu / Sl : 0.0) + (hi ? mu / Su : 0.0) +
+         P->o.kappa_d * mu * ((lo && !hi ? 1.0 : 0.0) - (hi && !lo ? 1.0 : 0.0));
+  }
+
+  // complementarity max |S z - mu_| over all bounds
+  __device__ double compl_max(double mu_) const {
+    double c = 0.0;
+    for (int i = lane; i < nw; i += WAVE) {
+      if (hasl(xl[i])) c = fmax(c, fabs((U[i] - xl[i]) * zl[i] - mu_));
+      if (hasu(xu[i])) c = fmax(c, fabs((xu[i] - U[i]) * zu[i] - mu_));
+    }
+    for (int r = lane; r < ng; r += WAVE) {
+      if (hasl(dl[r])) c = fmax(c, fabs((s[r] - dl[r]) * vl[r] - mu_));
+      if (hasu(du[r])) c = fmax(c, fabs((du[r] - s[r]) * vu[r] - mu_));
+    }
+    return wmax(c);
+  }
+
+  // filter
+  __device__ bool filter_ok(double phi, double th) const {
+    bool ok = true;
+    for (int e = lane; e < nfilt; e += WAVE) {
+      if (!(phi <= filt[2 * e] || th <= filt[2 * e + 1])) ok = false;
+    }
+    return !wany(!ok);
+  }
+  __device__ void filter_add(double phi, double th) {
+    // drop entries dominated by the new one, then append (IpFilter::AddEntry)
+    sync();
+    if (lane == 0) {
+      int w = 0;
+      for (int e = 0; e < nfilt; ++e) {
+        const double fp = filt[2 * e], ft = filt[2 * e + 1];
+        if (!(fp >= phi && ft >= th)) {
+          filt[2 * w] = fp; filt[2 * w + 1] = ft; ++w;
+        }
+      }
+      if (w >= FCAP) {  // capacity guard: drop the oldest entry
+        for (int e = 1; e < w; ++e) { filt[2 * e - 2] = filt[2 * e]; filt[2 * e - 1] = filt[2 * e + 1]; }
+        --w;
+      }
+      filt[2 * w] = phi; filt[2 * w + 1] = th;
+      filt[2 * FCAP] = (double)(w + 1);
+    }
+    sync();
+    nfilt = (int)filt[2 * FCAP];
+  }
+
+  // trial point u = U + a dUs, s = s + a dss: rollout into Xt, rows into dt.
+  // returns false on an evaluation error (NaN/Inf)
+  __device__ bool trial(double a, const double* dUs, const double* dss, double& ft, double& phit,
+                        double& tht) {
+    for (int i = lane; i < nw; i += WAVE) Ut[i] = U[i] + a * dUs[i];
+    sync();
+    rollout(Ut, Xt);
+    ft = df * eval_fg(Xt, dt, dc);
+    double th = 0.0;
+    bool bad = false;
+    for (int r = lane; r < ng; r += WAVE) {
+      const double sv = s[r] + a * dss[r];
+      th += fabs(dt[r] - sv);
+      if (!isfinite(dt[r])) bad = true;
+    }
+    tht = wsum(th);
+    bad = wany(bad) || !isfinite(ft);
+    if (bad) return false;
+    phit = barrier_obj(ft, Ut, s, dss, a);
+    return isfinite(phit);
+  }
+};
+
+// ------------------------------------------------------------------ kernel
+__global__ __launch_bounds__(WAVE) void nmpc_solve_kernel(const Params* __restrict__ prm, int B, IO io) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  const int b = blockIdx.x;
+  if (b >= B) return;
+  const int lane = threadIdx.x;
+  Solver S;
+  S.bind(prm, smem, lane, b);
+  const nmpc_options& o = prm->o;
+  const int N = S.N, nw = S.nw, ng = S.ng, m = S.m;
+  const int max_iter = o.max_iter;
+  double* trace = io.trace ? io.trace + (long long)b * (max_iter + 1) * TRACE_F : nullptr;
+
+  // ---------------- load scenario data
+  for (int i = lane; i < prm->np; i += WAVE) S.pp[i] = io.p[(long long)b * io.ld_p + i];
+  sync();
+  if (lane < S.nobs) {
+    S.obx[lane] = prm->oxp[lane] >= 0 ? S.pp[prm->oxp[lane]] : prm->ox[lane];
+    S.oby[lane] = prm->oyp[lane] >= 0 ? S.pp[prm->oyp[lane]] : prm->oy[lane];
+  }
+  const double brf = o.bound_relax_factor, cvt = o.constr_viol_tol;
+  bool invalid = false;
+  for (int i = lane; i < nw; i += WAVE) {
+    S.U[i] = io.x0[(long long)b * io.ld_x0 + i];
+    const double lo = io.lbx[(long long)b * io.ld_lbx + i], hi = io.ubx[(long long)b * io.ld_ubx + i];
+    S.xl[i] = lo > -BIGB ? lo - fmin(cvt, brf * fmax(1.0, fabs(lo))) : -INFINITY;
+    S.xu[i] = hi < BIGB ? hi + fmin(cvt, brf * fmax(1.0, fabs(hi))) : INFINITY;
+    if (lo > hi) invalid = true;
+  }
+  for (int r = lane; r < ng; r += WAVE) {
+    const double lo = io.lbg[(long long)b * io.ld_lbg + r], hi = io.ubg[(long long)b * io.ld_ubg + r];
+    S.dl[r] = lo > -BIGB ? lo - fmin(cvt, brf * fmax(1.0, fabs(lo))) : -INFINITY;  // unscaled for now
+    S.du[r] = hi < BIGB ? hi + fmin(cvt, brf * fmax(1.0, fabs(hi))) : INFINITY;
+    if (lo >= hi && lo > -BIGB) invalid = true;  // equality rows not supported
+    S.dc[r] = 1.0;
+  }
+  if (lane == 0) S.filt[2 * FCAP] = 0.0;
+  sync();
+  S.nfilt = 0;
+  S.delta = 0.0;
+  S.df = 1.0;
+  S.mu = o.mu_init;
+  int status = 0, it = 0;
+  if (wany(invalid)) {
+    status = ST_INVALID_PROBLEM;
+  }
+
+  // ---------------- scaling at the user's starting point (IPOPT gradient-based)
+  if (status == 0) {
+    S.rollout(S.U, S.X);
+    const double F0 = S.eval_fg(S.X, S.d, nullptr);
+    S.derivs(S.X, S.U);
+    S.adjoint(1.0, nullptr);
+    double gmax = 0.0;
+    bool bad = !isfinite(F0);
+    for (int i = lane; i < nw; i += WAVE) {
+      const double g = S.grad_u(i);
+      if (!isfinite(g)) bad = true;
+      gmax = fmax(gmax, fabs(g));
+    }
+    for (int r = lane; r < ng; r += WAVE)
+      if (!isfinite(S.d[r])) bad = true;
+    gmax = wmax(gmax);
+    if (wany(bad)) status = ST_INVALID_NUMBER;
+    double dfv = 1.0;
+    if (gmax > o.nlp_scaling_max_gradient) dfv = o.nlp_scaling_max_gradient / gmax;
+    S.df = fmax(dfv, o.nlp_scaling_min_value);
+    // Jacobian row maxima: J rows = G_k Z_k, Z_k[:,u_j] = (I + sum_{l=j+1}^{k-1} E_l) B_j
+    if (status == 0) {
+      const int k = lane;
+      double rmax[5 + NMPC_MAX_OBS];
+      for (int i = 0; i < m; ++i) rmax[i] = 0.0;
+      if (k <= N && k >= 1) {
+        const double* xk = S.X + k * 8;
+        double gxo[NMPC_MAX_OBS], gyo[NMPC_MAX_OBS];
+        for (int q = 0; q < S.nobs; ++q) {
+          const double ddx = xk[0] - S.obx[q], ddy = xk[1] - S.oby[q];
+          const double dd = sqrt(ddx * ddx + ddy * ddy);
+          gxo[q] = -(ddx / dd); gyo[q] = -(ddy / dd);
+        }
+        double e03 = 0, e04 = 0, e13 = 0, e14 = 0, e23 = 0;  // sums over l in (j, k)
+        const double T = S.T;
+        for (int j = k - 1; j >= 0; --j) {
+          double E03, E04, E13, E14, E23, b00, b10, b20;
+          S.stage_AB(j, E03, E04, E13, E14, E23, b00, b10, b20);
+          // rows z, theta, x5, x6, x7
+          rmax[0] = fmax(rmax[0], fmax(fabs(b20), fabs(T * e23)));
+          rmax[1] = fmax(rmax[1], fabs(T));
+          rmax[2] = fmax(rmax[2], fabs(T));
+          rmax[3] = fmax(rmax[3], fabs(T));
+          rmax[4] = fmax(rmax[4], fabs(T));
+          for (int q = 0; q < S.nobs; ++q) {
+            const double jv = gxo[q] * b00 + gyo[q] * b10;
+            const double jt = T * (gxo[q] * e03 + gyo[q] * e13);
+            const double jp = T * (gxo[q] * e04 + gyo[q] * e14);
+            rmax[5 + q] = fmax(rmax[5 + q], fmax(fabs(jv), fmax(fabs(jt), fabs(jp))));
+          }
+          e03 += E03; e04 += E04; e13 += E13; e14 += E14; e23 += E23;
+        }
+      }
+      double amax = 0.0;
+      for (int i = 0; i < m; ++i) amax = fmax(amax, rmax[i]);
+      amax = wmax(amax);
+      if (amax > o.nlp_scaling_max_gradient && k <= N) {
+        for (int i = 0; i < m; ++i) {
+          double dcv = rmax[i] > 0 ? fmin(1.0, o.nlp_scaling_max_gradient / rmax[i]) : 1.0;
+          S.dc[k * m + i] = fmax(dcv, o.nlp_scaling_min_value);
+        }
+      }
+      sync();
+    }
+  }
+
+  // ---------------- initial point
+  if (status == 0) {
+    for (int r = lane; r < ng; r += WAVE) {
+      S.dl[r] = S.dc[r] * S.dl[r];
+      S.du[r] = S.dc[r] * S.du[r];
+    }
+    int cx = 0, cs = 0;
+    const double kp = o.bound_push, kf_ = o.bound_frac;
+    for (int i = lane; i < nw; i += WAVE) {
+      const double lo = S.xl[i], hi = S.xu[i];
+      const bool hl = S.hasl(lo), hu = S.hasu(hi);
+      double x = S.U[i];
+      const double span = (hl && hu) ? hi - lo : INFINITY;
+      if (hl) x = fmax(x, lo + fmin(kp * fmax(1.0, fabs(lo)), kf_ * span));
+      if (hu) x = fmin(x, hi - fmin(kp * fmax(1.0, fabs(hi)), kf_ * span));
+      S.U[i] = x;
+      S.zl[i] = hl ? o.bound_mult_init_val : 0.0;
+      S.zu[i] = hu ? o.bound_mult_init_val : 0.0;
+      cx += (int)hl + (int)hu;
+    }
+    sync();
+    S.rollout(S.U, S.X);
+    S.eval_fg(S.X, S.d, S.dc);
+    S.derivs(S.X, S.U);
+    const double skp = o.slack_bound_push, skf = o.slack_bound_frac;
+    for (int r = lane; r < ng; r += WAVE) {
+      const double lo = S.dl[r], hi = S.du[r];
+      const bool hl = S.hasl(lo), hu = S.hasu(hi);
+      double x = S.d[r];
+      const double span = (hl && hu) ? hi - lo : INFINITY;
+      if (hl) x = fmax(x, lo + fmin(skp * fmax(1.0, fabs(lo)), skf * span));
+      if (hu) x = fmin(x, hi - fmin(skp * fmax(1.0, fabs(hi)), skf * span));
+      S.s[r] = x;
+      S.vl[r] = hl ? o.bound_mult_init_val : 0.0;
+      S.vu[r] = hu ? o.bound_mult_init_val : 0.0;
+      S.y[r] = 0.0;
+      cs += (int)hl + (int)hu;
+    }
+    S.nzx = (int)wsum((double)cx);
+    S.nzs = (int)wsum((double)cs);
+    sync();
+    // least-squares constraint multipliers: (I + J^T J) wx = bx + J^T bs ; y = bs - J wx
+    if (o.constr_mult_init_max > 0 && ng > 0) {
+      for (int i = lane; i < nw; i += WAVE) { S.sigx[i] = 1.0; S.ru[i] = S.zl[i] - S.zu[i]; }
+      S.delta = 0.0;
+      S.summaries(SUM_LS);
+      S.riccati(0.0, -S.df, false, S.sigx, S.ru);
+      S.forward(S.dU, S.dX);
+      double ymax = 0.0;
+      for (int r = lane; r < ng; r += WAVE) {
+        // y = bs - J wx with J wx = Gt dX
+        const int k = r / m, i = r - k * m;
+        const double* xk = S.X + k * 8;
+        const double* dxk = S.dX + k * 8;
+        double jd;
+        if (i < 5) jd = S.dc[r] * dxk[boxidx(i)];
+        else {
+          const int q = i - 5;
+          const double ddx = xk[0] - S.obx[q], ddy = xk[1] - S.oby[q];
+          const double dd = sqrt(ddx * ddx + ddy * ddy);
+          jd = S.dc[r] * ((-(ddx / dd)) * dxk[0] + (-(ddy / dd)) * dxk[1]);
+        }
+        const double yv = (S.vu[r] - S.vl[r]) - jd;
+        S.y[r] = yv;
+        ymax = fmax(ymax, fabs(yv));
+      }
+      ymax = wmax(ymax);
+      sync();
+      if (!(ymax <= o.constr_mult_init_max)) {
+        for (int r = lane; r < ng; r += WAVE) S.y[r] = 0.0;
+      }
+      sync();
+    }
+  }
+
+  // ---------------- main loop
+  double f = 0.0;
+  if (status == 0) {
+    f = S.df * S.eval_fg(S.X, S.d, S.dc);
+  }
+  S.mu = o.mu_init;
+  S.tau = fmax(o.tau_min, 1.0 - S.mu);
+  double theta_max = -1.0, theta_min = -1.0;
+  double delta_last = 0.0, delta_curr = 0.0;
+  bool in_soft = false, tiny_flag = false;
+  int soft_cnt = 0, acc_cnt = 0, last_obj_iter = -1;
+  double last_obj = -1e50, curr_obj = -1e50;
+  const double smax = o.s_max;
+  bool running = (status == 0);
+
+  while (running) {
+    // ===== adjoint with current y (grad of the Lagrangian, Hessian multipliers)
+    S.adjoint(S.df, S.y);
+    // ===== optimality error (IpoptCalculatedQuantities::curr_nlp_error)
+    double dinf = 0, cviol = 0, ucviol = 0, cmp = 0, sumy = 0, sumz = 0, sumv = 0, pinf = 0;
+    bool bad = false;
+    for (int i = lane; i < nw; i += WAVE) {
+      const double g = S.grad_u(i) - S.zl[i] + S.zu[i];
+      if (!isfinite(g)) bad = true;
+      dinf = fmax(dinf, fabs(g));
+      if (S.hasl(S.xl[i])) cmp = fmax(cmp, fabs((S.U[i] - S.xl[i]) * S.zl[i]));
+      if (S.hasu(S.xu[i])) cmp = fmax(cmp, fabs((S.xu[i] - S.U[i]) * S.zu[i]));
+      sumz += fabs(S.zl[i]) + fabs(S.zu[i]);
+    }
+    for (int r = lane; r < ng; r += WAVE) {
+      const double g = -S.y[r] - S.vl[r] + S.vu[r];
+      dinf = fmax(dinf, fabs(g));
+      double cv = 0.0;
+      if (S.hasl(S.dl[r])) {
+        cv = fmax(cv, S.dl[r] - S.d[r]);
+        cmp = fmax(cmp, fabs((S.s[r] - S.dl[r]) * S.vl[r]));
+      }
+      if (S.hasu(S.du[r])) {
+        cv = fmax(cv, S.d[r] - S.du[r]);
+        cmp = fmax(cmp, fabs((S.du[r] - S.s[r]) * S.vu[r]));
+      }
+      cviol = fmax(cviol, cv);
+      ucviol = fmax(ucviol, cv / S.dc[r]);
+      pinf = fmax(pinf, fabs(S.d[r] - S.s[r]));
+      sumy += fabs(S.y[r]);
+      sumv += fabs(S.vl[r]) + fabs(S.vu[r]);
+      if (!isfinite(S.d[r]) || !isfinite(g)) bad = true;
+    }
+    dinf = wmax(dinf); cviol = wmax(cviol); ucviol = wmax(ucviol); cmp = wmax(cmp);
+    pinf = wmax(pinf);
+    sumy = wsum(sumy); sumz = wsum(sumz); sumv = wsum(sumv);
+    bad = wany(bad) || !isfinite(f);
+    const int nd = ng + S.nzx + S.nzs, nc = S.nzx + S.nzs;
+    double sd = nd ? (sumy + sumz + sumv) / nd : 0.0;
+    sd = fmax(smax, sd) / smax;
+    double sc = nc ? (sumz + sumv) / nc : 0.0;
+    sc = fmax(smax, sc) / smax;
+    const double err = fmax(fmax(dinf / sd, cviol), cmp / sc);
+    if (bad || !isfinite(err)) { status = ST_INVALID_NUMBER; break; }
+    const double u_dinf = dinf / S.df, u_cmp = cmp / S.df;
+    if (err <= o.tol && u_dinf <= o.dual_inf_tol && ucviol <= o.constr_viol_tol && u_cmp <= o.compl_inf_tol) {
+      status = ST_SUCCESS; break;
+    }
+    if (it != last_obj_iter) { last_obj = curr_obj; curr_obj = f; last_obj_iter = it; }
+    const bool acceptable = err <= o.acceptable_tol && u_dinf <= o.acceptable_dual_inf_tol &&
+                            ucviol <= o.acceptable_constr_viol_tol && u_cmp <= o.acceptable_compl_inf_tol &&
+                            fabs(curr_obj - last_obj) / fmax(1.0, fabs(curr_obj)) <= o.acceptable_obj_change_tol;
+    if (o.acceptable_iter > 0 && acceptable) {
+      if (++acc_cnt >= o.acceptable_iter) { status = ST_ACCEPTABLE; break; }
+    } else {
+      acc_cnt = 0;
+    }
+    if (it >= max_iter) { status = ST_MAXITER; break; }
+
+    // ===== monotone barrier update (MonotoneMuUpdate::UpdateBarrierParameter)
+    {
+      const double base = fmax(dinf / sd, pinf);
+      double sub = fmax(base, S.compl_max(S.mu) / sc);
+      bool done = false, tsf = tiny_flag;
+      while ((sub <= o.barrier_tol_factor * S.mu || tsf) && !done) {
+        double nmu = fmin(o.kappa_mu * S.mu, pow(S.mu, o.theta_mu));
+        nmu = fmax(nmu, fmin(o.tol, o.compl_inf_tol) / (o.barrier_tol_factor + 1.0));
+        const bool changed = nmu != S.mu;
+        if (!changed && tsf) { status = ST_TINY; break; }
+        S.mu = nmu;
+        S.tau = fmax(o.tau_min, 1.0 - S.mu);
+        if (!changed) done = true;
+        else {
+          sub = fmax(base, S.compl_max(S.mu) / sc);
+          done = sub > o.barrier_tol_factor * S.mu;
+        }
+        if (done && changed) { S.nfilt = 0; in_soft = false; }
+        tsf = false;
+      }
+      if (status != 0) break;
+      tiny_flag = false;
+    }
+    const double mu = S.mu, tau = S.tau;
+
+    // ===== search direction with inertia correction (PDPerturbationHandler)
+    for (int i = lane; i < nw; i += WAVE) {
+      const bool hl = S.hasl(S.xl[i]), hu = S.hasu(S.xu[i]);
+      const double Sl = hl ? S.U[i] - S.xl[i] : 1.0, Su = hu ? S.xu[i] - S.U[i] : 1.0;
+      S.sigx[i] = (hl ? S.zl[i] / Sl : 0.0) + (hu ? S.zu[i] / Su : 0.0);
+      S.ru[i] = -(hl ? mu / Sl : 0.0) + (hu ? mu / Su : 0.0) +
+                o.kappa_d * mu * ((hl && !hu ? 1.0 : 0.0) - (hu && !hl ? 1.0 : 0.0));
+    }
+    sync();
+    if (delta_curr > 0) delta_last = delta_curr;
+    double delta = 0.0;
+    bool fact_ok = false;
+    while (true) {
+      S.delta = delta;
+      S.summaries(SUM_NEWTON);
+      if (S.riccati(S.df, S.df, true, S.sigx, S.ru)) { fact_ok = true; break; }
+      sync();
+      if (delta == 0.0) {
+        delta = (delta_last == 0.0) ? o.first_hessian_perturbation
+                                    : fmax(o.min_hessian_perturbation, delta_last * o.perturb_dec_fact);
+      } else {
+        if (delta_last == 0.0 || 1e5 * delta_last < delta) delta *= o.perturb_inc_fact_first;
+        else delta *= o.perturb_inc_fact;
+      }
+      if (delta > o.max_hessian_perturbation) break;
+    }
+    delta_curr = delta;
+    S.delta = delta;
+    if (!fact_ok) { status = ST_STEP_ERR; break; }
+    S.forward(S.dU, S.dX);
+    S.row_step(S.dX, nullptr, false, S.ds);
+
+    // ===== line search (BacktrackingLineSearch + FilterLSAcceptor)
+    double theta_ref = 0.0, gbd = 0.0;
+    {
+      double th = 0.0, g = 0.0;
+      for (int r = lane; r < ng; r += WAVE) {
+        th += fabs(S.d[r] - S.s[r]);
+        const bool hl = S.hasl(S.dl[r]), hu = S.hasu(S.du[r]);
+        const double gs = -(hl ? mu / (S.s[r] - S.dl[r]) : 0.0) + (hu ? mu / (S.du[r] - S.s[r]) : 0.0) +
+                          o.kappa_d * mu * ((hl && !hu ? 1.0 : 0.0) - (hu && !hl ? 1.0 : 0.0));
+        g += gs * S.ds[r];
+      }
+      for (int i = lane; i < nw; i += WAVE) g += S.ru[i] * S.dU[i];
+      if (lane <= N) {
+        double gx = 0.0;
+#pragma unroll
+        for (int c = 0; c < 8; ++c) gx += S.gl[lane * 8 + c] * S.dX[lane * 8 + c];
+        g += S.df * gx;
+      }
+      theta_ref = wsum(th);
+      gbd = wsum(g);
+    }
+    const double phi_ref = S.barrier_obj(f, S.U, S.s, nullptr, 0.0);
+    if (theta_max < 0) {
+      theta_max = o.theta_max_fact * fmax(1.0, theta_ref);
+      theta_min = o.theta_min_fact * fmax(1.0, theta_ref);
+    }
+    const double eps = 2.220446049250313e-16;
+    auto cmp_le = [&](double lhs, double rhs, double bas) { return lhs - rhs <= 10.0 * eps * fabs(bas); };
+    auto is_ftype = [&](double a) {
+      return gbd < 0.0 && a * pow(-gbd, o.s_phi) > o.delta * pow(theta_ref, o.s_theta);
+    };
+    auto armijo = [&](double a, double phit) { return cmp_le(phit - phi_ref, o.eta_phi * a * gbd, phi_ref); };
+    auto acc_iter = [&](double phit, double tht) {
+      if (phit > phi_ref) {
+        double basval = 1.0;
+        if (fabs(phi_ref) > 10.0) basval = log10(fabs(phi_ref));
+        if (log10(phit - phi_ref) > o.obj_max_inc + basval) return false;
+      }
+      return cmp_le(tht, (1.0 - o.gamma_theta) * theta_ref, theta_ref) ||
+             cmp_le(phit - phi_ref, -o.gamma_phi * theta_ref, phi_ref);
+    };
+    auto check_accept = [&](double a_test, double phit, double tht) {
+      if (tht > theta_max) return false;
+      bool ok;
+      if (a_test > 0.0 && is_ftype(a_test) && theta_ref <= theta_min) ok = armijo(a_test, phit);
+      else ok = acc_iter(phit, tht);
+      if (!ok) return false;
+      return S.filter_ok(phit, tht);
+    };
+
+    // accepted step bookkeeping: which step vectors, alphas
+    int acc_kind = 0;  // 0 none, 1 regular (dU/ds), 2 regular SOC (dU2/ds2), 3 soft
+    double alpha_p = 0.0, alpha_d = 0.0, f_acc = 0.0;
+    int ls_trials = 0;
+    double a_test_acc = 0.0, phi_acc = 0.0;
+
+    // soft restoration step (BacktrackingLineSearch::TrySoftRestoStep); returns
+    // 0 rejected, 1 accepted, 2 accepted & satisfies the original criterion
+    auto try_soft = [&]() -> int {
+      const double ap = S.frac_to_bound(tau, S.dU, S.ds);
+      const double ad = S.dual_frac_to_bound(tau, S.dU, S.ds);
+      const double a = fmin(ap, ad);
+      // current pd error (grad_lag from the adjoint computed at loop start)
+      double dual = 0, prim = 0, cm = 0;
+      for (int i = lane; i < nw; i += WAVE) {
+        dual += fabs(S.grad_u(i) - S.zl[i] + S.zu[i]);
+        if (S.hasl(S.xl[i])) cm += fabs((S.U[i] - S.xl[i]) * S.zl[i] - mu);
+        if (S.hasu(S.xu[i])) cm += fabs((S.xu[i] - S.U[i]) * S.zu[i] - mu);
+      }
+      for (int r = lane; r < ng; r += WAVE) {
+        dual += fabs(-S.y[r] - S.vl[r] + S.vu[r]);
+        prim += fabs(S.d[r] - S.s[r]);
+        if (S.hasl(S.dl[r])) cm += fabs((S.s[r] - S.dl[r]) * S.vl[r] - mu);
+        if (S.hasu(S.du[r])) cm += fabs((S.du[r] - S.s[r]) * S.vu[r] - mu);
+      }
+      const double nn = (double)(nw + ng);
+      const double e_c = wsum(dual) / nn + (ng ? wsum(prim) / ng : 0.0) + (nc ? wsum(cm) / nc : 0.0);
+      double ft, phit, tht;
+      ++ls_trials;
+      if (!S.trial(a, S.dU, S.ds, ft, phit, tht)) return 0;
+      // trial multipliers into the "2" buffers: dU2 <- (unused) ; stage them in place later
+      // evaluate grad_lag at the trial point: derivatives + adjoint with trial y
+      // (overwrites the current derivative data; if rejected the solve stops)
+      for (int r = lane; r < ng; r += WAVE) {
+        double D, rs;
+        S.row_rs(r, D, rs);
+        S.dms[r] = S.y[r] + a * (D * S.ds[r] + rs);  // trial y
+      }
+      sync();
+      S.derivs(S.Xt, S.Ut);
+      // adjoint at the trial point: swap X temporarily
+      double* Xs = S.X; S.X = S.Xt;
+      S.adjoint(S.df, S.dms);
+      S.X = Xs;
+      double dual2 = 0, prim2 = 0, cm2 = 0;
+      for (int i = lane; i < nw; i += WAVE) {
+        double dzl, dzu;
+        S.dz_x(i, S.dU[i], dzl, dzu);
+        const double zlt = S.zl[i] + a * dzl, zut = S.zu[i] + a * dzu;
+        dual2 += fabs(S.grad_u(i) - zlt + zut);
+        if (S.hasl(S.xl[i])) cm2 += fabs((S.Ut[i] - S.xl[i]) * zlt - mu);
+        if (S.hasu(S.xu[i])) cm2 += fabs((S.xu[i] - S.Ut[i]) * zut - mu);
+      }
+      for (int r = lane; r < ng; r += WAVE) {
+        double dvl, dvu;
+        S.dv_s(r, S.ds[r], dvl, dvu);
+        const double vlt = S.vl[r] + a * dvl, vut = S.vu[r] + a * dvu;
+        const double sv = S.s[r] + a * S.ds[r];
+        dual2 += fabs(-S.dms[r] - vlt + vut);
+        prim2 += fabs(S.dt[r] - sv);
+        if (S.hasl(S.dl[r])) cm2 += fabs((sv - S.dl[r]) * vlt - mu);
+        if (S.hasu(S.du[r])) cm2 += fabs((S.du[r] - sv) * vut - mu);
+      }
+      const double e_t = wsum(dual2) / nn + (ng ? wsum(prim2) / ng : 0.0) + (nc ? wsum(cm2) / nc : 0.0);
+      if (e_t <= o.soft_resto_pderror_reduction_factor * e_c) {
+        alpha_p = a; alpha_d = a; f_acc = ft;
+        acc_kind = 3;
+        return check_accept(0.0, phit, tht) ? 2 : 1;
+      }
+      return 0;
+    };
+
+    bool derivs_done = false;  // soft-resto path already computed derivatives at the trial
+    if (in_soft) {
+      ++soft_cnt;
+      if (soft_cnt <= o.max_soft_resto_iters) {
+        const int r = try_soft();
+        if (r > 0) derivs_done = true;
+        if (r == 2) in_soft = false;
+      }
+    } else {
+      // tiny step detection (BacktrackingLineSearch::DetectTinyStep)
+      double mx = 0.0, msv = 0.0;
+      for (int i = lane; i < nw; i += WAVE) mx = fmax(mx, fabs(S.dU[i] / (1.0 + fabs(S.U[i]))));
+      for (int r = lane; r < ng; r += WAVE) msv = fmax(msv, fabs(S.ds[r] / (1.0 + fabs(S.s[r]))));
+      mx = wmax(mx); msv = wmax(msv);
+      const bool tiny = mx <= o.tiny_step_tol && msv <= o.tiny_step_tol && pinf <= 1e-4;
+      if (tiny) {
+        const double a = S.frac_to_bound(tau, S.dU, S.ds);
+        double ft, phit, tht;
+        ++ls_trials;
+        if (S.trial(a, S.dU, S.ds, ft, phit, tht)) {
+          acc_kind = 1; alpha_p = a; f_acc = ft;
+          tiny_flag = true;
+        }
+      } else {
+        double amin = o.gamma_theta;
+        if (gbd < 0) {
+          amin = fmin(o.gamma_theta, o.gamma_phi * theta_ref / (-gbd));
+          if (theta_ref <= theta_min)
+            amin = fmin(amin, o.delta * pow(theta_ref, o.s_theta) / pow(-gbd, o.s_phi));
+        }
+        amin *= o.alpha_min_frac;
+        const double amax_p = S.frac_to_bound(tau, S.dU, S.ds);
+        double a = amax_p;
+        int n_steps = 0;
+        while (a > amin || n_steps == 0) {
+          double ft, phit, tht;
+          ++ls_trials;
+          const bool okev = S.trial(a, S.dU, S.ds, ft, phit, tht);
+          if (okev && check_accept(a, phit, tht)) {
+            acc_kind = 1; alpha_p = a; f_acc = ft; a_test_acc = a; phi_acc = phit;
+            break;
+          }
+          if (okev && a == amax_p && theta_ref <= tht && o.max_soc > 0) {
+            // second-order correction (FilterLSAcceptor::TrySecondOrderCorrection)
+            double th_tr = tht, th_old = 0.0, a_soc = a;
+            for (int r = lane; r < ng; r += WAVE) S.dms[r] = S.d[r] - S.s[r];
+            int cnt = 0;
+            bool soc_acc = false;
+            const double* dsp = S.ds;  // step whose trial is in Ut/dt
+            while (cnt < o.max_soc && (cnt == 0 || th_tr <= o.kappa_soc * th_old)) {
+              th_old = th_tr;
+              for (int r = lane; r < ng; r += WAVE) {
+                const double sv = S.s[r] + a_soc * dsp[r];
+                S.dms[r] = a_soc * S.dms[r] + (S.dt[r] - sv);
+              }
+              sync();
+              S.summaries(SUM_SOC);
+              S.resolve(S.df, S.ru);
+              S.forward(S.dU2, S.dX2);
+              S.row_step(S.dX2, S.dms, true, S.ds2);
+              a_soc = S.frac_to_bound(tau, S.dU2, S.ds2);
+              dsp = S.ds2;
+              double ft2, phit2, tht2;
+              ++ls_trials;
+              if (!S.trial(a_soc, S.dU2, S.ds2, ft2, phit2, tht2)) break;
+              if (check_accept(a, phit2, tht2)) {
+                acc_kind = 2; alpha_p = a_soc; f_acc = ft2; a_test_acc = a; phi_acc = phit2;
+                soc_acc = true;
+                break;
+              }
+              ++cnt;
+              th_tr = tht2;
+            }
+            if (soc_acc) break;
+          }
+          a *= o.alpha_red_factor;
+          ++n_steps;
+        }
+        if (acc_kind == 0) {
+          const int r = try_soft();
+          if (r > 0) derivs_done = true;
+          if (r == 1) { in_soft = true; soft_cnt = 0; }
+        } else {
+          if (!(is_ftype(a_test_acc) && armijo(a_test_acc, phi_acc)))
+            S.filter_add(phi_ref - o.gamma_phi * theta_ref, (1.0 - o.gamma_theta) * theta_ref);
+        }
+      }
+    }
+    if (acc_kind == 0) { status = ST_RESTO_FAIL; break; }
+
+    // ===== accept the trial point (IpoptAlgorithm::AcceptTrialPoint)
+    {
+      const double* dUa = (acc_kind == 2) ? S.dU2 : S.dU;
+      const double* dsa = (acc_kind == 2) ? S.ds2 : S.ds;
+      if (acc_kind != 3) alpha_d = S.dual_frac_to_bound(tau, dUa, dsa);
+      const double ap = alpha_p, ad = alpha_d;
+      const double ks = o.kappa_sigma;
+      // bound multipliers of U (old slacks for the step, new slacks for kappa_sigma)
+      for (int i = lane; i < nw; i += WAVE) {
+        double dzl, dzu;
+        S.dz_x(i, dUa[i], dzl, dzu);
+        double nzl = S.zl[i] + ad * dzl, nzu = S.zu[i] + ad * dzu;
+        const double un = S.Ut[i];
+        if (S.hasl(S.xl[i])) { const double Sn = un - S.xl[i]; nzl = fmax(fmin(nzl, ks * mu / Sn), mu / (ks * Sn)); }
+        else nzl = 0.0;
+        if (S.hasu(S.xu[i])) { const double Sn = S.xu[i] - un; nzu = fmax(fmin(nzu, ks * mu / Sn), mu / (ks * Sn)); }
+        else nzu = 0.0;
+        S.zl[i] = nzl; S.zu[i] = nzu;
+      }
+      for (int r = lane; r < ng; r += WAVE) {
+        double D, rs, dvl, dvu;
+        S.row_rs(r, D, rs);
+        S.dv_s(r, dsa[r], dvl, dvu);
+        const double dyv = D * dsa[r] + rs;
+        const double sn = S.s[r] + ap * dsa[r];
+        double nvl = S.vl[r] + ad * dvl, nvu = S.vu[r] + ad * dvu;
+        if (S.hasl(S.dl[r])) { const double Sn = sn - S.dl[r]; nvl = fmax(fmin(nvl, ks * mu / Sn), mu / (ks * Sn)); }
+        else nvl = 0.0;
+        if (S.hasu(S.du[r])) { const double Sn = S.du[r] - sn; nvu = fmax(fmin(nvu, ks * mu / Sn), mu / (ks * Sn)); }
+        else nvu = 0.0;
+        S.y[r] = S.y[r] + ap * dyv;
+        S.vl[r] = nvl; S.vu[r] = nvu;
+        S.s[r] = sn;
+        S.d[r] = S.dt[r];
+      }
+      for (int i = lane; i < nw; i += WAVE) S.U[i] = S.Ut[i];
+      if (lane <= N) {
+#pragma unroll
+        for (int c = 0; c < 8; ++c) S.X[lane * 8 + c] = S.Xt[lane * 8 + c];
+      }
+      sync();
+      f = f_acc;
+      if (!derivs_done) S.derivs(S.X, S.U);
+      else {
+        // soft resto computed derivatives at the trial; trig uses U (same values)
+        sync();
+      }
+    }
+    ++it;
+    if (trace && lane == 0) {
+      double th = 0.0;
+      for (int r = 0; r < ng; ++r) th += fabs(S.d[r] - S.s[r]);
+      double* t = trace + (long long)(it - 1) * TRACE_F;
+      t[0] = it; t[1] = mu; t[2] = f; t[3] = th; t[4] = delta_curr; t[5] = alpha_p; t[6] = alpha_d;
+      t[7] = ls_trials;
+    }
+    sync();
+  }
+
+  // ---------------- outputs (honor_original_bounds)
+  for (int i = lane; i < nw; i += WAVE) {
+    const double lo = io.lbx[(long long)b * io.ld_lbx + i], hi = io.ubx[(long long)b * io.ld_ubx + i];
+    S.Ut[i] = fmin(fmax(S.U[i], lo), hi);
+  }
+  sync();
+  S.rollout(S.Ut, S.Xt);
+  const double fo = S.eval_fg(S.Xt, S.dt, nullptr);
+  for (int i = lane; i < nw; i += WAVE) {
+    io.x_out[(long long)b * nw + i] = S.Ut[i];
+    if (io.lam_x) io.lam_x[(long long)b * nw + i] = (S.zu[i] - S.zl[i]) / S.df;
+  }
+  for (int r = lane; r < ng; r += WAVE) {
+    if (io.g_out) io.g_out[(long long)b * ng + r] = S.dt[r];
+    if (io.lam_g) io.lam_g[(long long)b * ng + r] = S.y[r] * S.dc[r] / S.df;
+  }
+  if (io.X_out) {
+    const int nX = prm->nX;
+    for (int i = lane; i < nX; i += WAVE) io.X_out[(long long)b * nX + i] = S.Xt[i];
+  }
+  if (lane == 0) {
+    if (io.f_out) io.f_out[b] = fo;
+    if (io.status) io.status[b] = status;
+    if (io.iters) io.iters[b] = it;
+  }
+}
+
+// closed-loop shift kernel (Python/NMPC_TT.py:13-30): one thread per scenario
+__global__ void nmpc_shift_kernel(int B, int N, int np, double T, double* p, long long ld_p,
+                                  const double* u, double* w_out, const double* vt, const double* wt) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  double* pb = p + (long long)b * ld_p;
+  const double* ub = u + (long long)b * 6 * N;
+  const double th = pb[3], ps = pb[4], v = ub[0];
+  const double f0 = v * cos(ps) * cos(th), f1 = v * sin(ps) * cos(th), f2 = v * sin(th);
+  pb[0] = pb[0] + T * f0; pb[1] = pb[1] + T * f1; pb[2] = pb[2] + T * f2;
+  for (int c = 0; c < 5; ++c) pb[3 + c] = pb[3 + c] + T * ub[1 + c];
+  double* wb = w_out + (long long)b * 6 * N;
+  for (int k = 0; k < N; ++k) {
+    const int src = (k + 1 < N) ? k + 1 : N - 1;
+    for (int c = 0; c < 6; ++c) wb[k * 6 + c] = ub[src * 6 + c];
+  }
+  const double xs2 = pb[10];
+  const double vv = vt[b], ww = wt[b];
+  pb[8] = pb[8] + T * (vv * cos(xs2));
+  pb[9] = pb[9] + T * (vv * sin(xs2));
+  pb[10] = pb[10] + T * ww;
+  (void)np;
+}
+
+// ------------------------------------------------------------------ host side
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+}  // namespace
+
+struct nmpc_handle {
+  Params hp;
+  Params* dprm = nullptr;
+  int device = 0;
+  int lds_bytes = 0;
+  // staging buffers for the host-pointer API
+  double* dbuf = nullptr;
+  size_t dbuf_bytes = 0;
+  int* ibuf = nullptr;
+  size_t ibuf_bytes = 0;
+  bool trace = false;
+  double* dtrace = nullptr;
+  size_t trace_bytes = 0;
+  int last_B = 0;
+};
+
+static int layout(Params& P) {
+  int off = 0;
+  auto al = [&](int n) { int o = off; off += (n + 1) & ~1; return o; };
+  const int nw = P.nw, ng = P.ng, nX = P.nX, NS = P.N + 1;
+  P.U = al(nw); P.Ut = al(nw); P.dU = al(nw); P.dU2 = al(nw); P.zl = al(nw); P.zu = al(nw);
+  P.xl = al(nw); P.xu = al(nw); P.sigx = al(nw); P.ru = al(nw);
+  P.X = al(nX); P.Xt = al(nX); P.dX = al(nX); P.dX2 = al(nX);
+  P.s = al(ng); P.y = al(ng); P.vl = al(ng); P.vu = al(ng); P.d = al(ng); P.dt = al(ng);
+  P.ds = al(ng); P.ds2 = al(ng); P.dc = al(ng); P.dl = al(ng); P.du = al(ng); P.dms = al(ng);
+  P.gl = al(8 * NS); P.Hl = al(21 * NS); P.trig = al(8 * NS); P.st = al(16 * NS); P.lam = al(8 * NS);
+  P.K = al(48 * P.N); P.kf = al(6 * P.N); P.Lc = al(28 * P.N);
+  P.P0 = al(64); P.P1 = al(64); P.pv0 = al(8); P.pv1 = al(8); P.PA = al(64); P.BtP = al(48); P.St = al(48);
+  P.p = al(64); P.ob = al(2 * NMPC_MAX_OBS); P.inc = al(8 * 64); P.filt = al(2 * FCAP + 2); P.red = al(64);
+  P.total = off;
+  return off * 8;
+}
+
+extern "C" {
+
+void nmpc_default_options(nmpc_options* o) {
+  std::memset(o, 0, sizeof(*o));
+  o->max_iter = 3000; o->acceptable_iter = 15; o->max_soc = 4; o->max_soft_resto_iters = 10;
+  o->tol = 1e-8; o->acceptable_tol = 1e-6; o->acceptable_obj_change_tol = 1e20;
+  o->acceptable_dual_inf_tol = 1e10; o->acceptable_constr_viol_tol = 1e-2; o->acceptable_compl_inf_tol = 1e-2;
+  o->dual_inf_tol = 1.0; o->constr_viol_tol = 1e-4; o->compl_inf_tol = 1e-4;
+  o->mu_init = 0.1; o->kappa_mu = 0.2; o->theta_mu = 1.5; o->barrier_tol_factor = 10.0; o->tau_min = 0.99;
+  o->bound_push = 1e-2; o->bound_frac = 1e-2; o->slack_bound_push = 1e-2; o->slack_bound_frac = 1e-2;
+  o->bound_relax_factor = 1e-8; o->bound_mult_init_val = 1.0; o->constr_mult_init_max = 1e3;
+  o->nlp_scaling_max_gradient = 100.0; o->nlp_scaling_min_value = 1e-8; o->kappa_d = 1e-5;
+  o->kappa_sigma = 1e10; o->s_max = 100.0;
+  o->theta_max_fact = 1e4; o->theta_min_fact = 1e-4; o->gamma_theta = 1e-5; o->gamma_phi = 1e-8;
+  o->delta = 1.0; o->s_theta = 1.1; o->s_phi = 2.3; o->eta_phi = 1e-8;
+  o->alpha_red_factor = 0.5; o->alpha_min_frac = 0.05; o->kappa_soc = 0.99; o->obj_max_inc = 5.0;
+  o->first_hessian_perturbation = 1e-4; o->min_hessian_perturbation = 1e-20; o->max_hessian_perturbation = 1e20;
+  o->perturb_inc_fact_first = 100.0; o->perturb_inc_fact = 8.0; o->perturb_dec_fact = 1.0 / 3.0;
+  o->tiny_step_tol = 10 * 2.220446049250313e-16; o->soft_resto_pderror_reduction_factor = 0.9999;
+}
+
+const char* nmpc_last_error(void) { return g_err.c_str(); }
+
+int nmpc_create(const nmpc_desc* desc, nmpc_handle** out) {
+  if (!desc || !out) return fail(NMPC_E_INVALID, "null argument");
+  if (desc->model != NMPC_MODEL_UAV8G) return fail(NMPC_E_INVALID, "unsupported model");
+  if (desc->N < 1 || desc->N > NMPC_MAX_N) return fail(NMPC_E_INVALID, "N out of range [1,63]");
+  if (desc->n_obs < 0 || desc->n_obs > NMPC_MAX_OBS) return fail(NMPC_E_INVALID, "n_obs out of range");
+  if (desc->np < 11 || desc->np > 64) return fail(NMPC_E_INVALID, "np out of range [11,64]");
+  if (!(desc->T > 0)) return fail(NMPC_E_INVALID, "T must be positive");
+  if (desc->opts.max_iter < 0 || desc->opts.max_iter > FCAP - 1 + 100000)
+    return fail(NMPC_E_INVALID, "bad max_iter");
+  for (int j = 0; j < desc->n_obs; ++j) {
+    if (desc->obs_x_pidx[j] >= desc->np || desc->obs_y_pidx[j] >= desc->np)
+      return fail(NMPC_E_INVALID, "obstacle parameter index >= np");
+  }
+  nmpc_handle* h = new nmpc_handle();
+  Params& P = h->hp;
+  std::memset(&P, 0, sizeof(P));
+  P.N = desc->N; P.nobs = desc->n_obs; P.m = 5 + desc->n_obs; P.np = desc->np;
+  P.nw = 6 * P.N; P.ng = P.m * (P.N + 1); P.nX = 8 * (P.N + 1);
+  P.T = desc->T; P.w1 = desc->w1; P.w2 = desc->w2; P.hv = desc->vfov / 2; P.hh = desc->hfov / 2;
+  for (int j = 0; j < NMPC_MAX_OBS; ++j) {
+    P.oxp[j] = -1; P.oyp[j] = -1;
+  }
+  for (int j = 0; j < desc->n_obs; ++j) {
+    P.ox[j] = desc->obs_x[j]; P.oy[j] = desc->obs_y[j]; P.orr[j] = desc->obs_rsum[j];
+    P.oxp[j] = desc->obs_x_pidx[j]; P.oyp[j] = desc->obs_y_pidx[j];
+  }
+  P.o = desc->opts;
+  h->lds_bytes = layout(P);
+  if (h->lds_bytes > 160 * 1024) {
+    delete h;
+    return fail(NMPC_E_INVALID, "problem too large for the LDS-resident kernel (N*(5+n_obs) too big)");
+  }
+  if (hipGetDevice(&h->device) != hipSuccess) { delete h; return fail(NMPC_E_HIP, "hipGetDevice failed"); }
+  if (hipMalloc(&h->dprm, sizeof(Params)) != hipSuccess) { delete h; return fail(NMPC_E_NOMEM, "hipMalloc params"); }
+  if (hipMemcpy(h->dprm, &P, sizeof(Params), hipMemcpyHostToDevice) != hipSuccess) {
+    hipFree(h->dprm); delete h; return fail(NMPC_E_HIP, "hipMemcpy params");
+  }
+  if (hipFuncSetAttribute((const void*)nmpc_solve_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                          h->lds_bytes) != hipSuccess) {
+    hipFree(h->dprm); delete h; return fail(NMPC_E_HIP, "hipFuncSetAttribute(MaxDynamicSharedMemorySize)");
+  }
+  *out = h;
+  return NMPC_OK;
+}
+
+int nmpc_destroy(nmpc_handle* h) {
+  if (!h) return NMPC_OK;
+  if (h->dprm) hipFree(h->dprm);
+  if (h->dbuf) hipFree(h->dbuf);
+  if (h->ibuf) hipFree(h->ibuf);
+  if (h->dtrace) hipFree(h->dtrace);
+  delete h;
+  return NMPC_OK;
+}
+
+int nmpc_dims(const nmpc_handle* h, int32_t* nw, int32_t* ng, int32_t* np, int32_t* nX) {
+  if (!h) return fail(NMPC_E_INVALID, "null handle");
+  if (nw) *nw = h->hp.nw;
+  if (ng) *ng = h->hp.ng;
+  if (np) *np = h->hp.np;
+  if (nX) *nX = h->hp.nX;
+  return NMPC_OK;
+}
+
+int nmpc_kernel_info(const nmpc_handle* h, int32_t* lds_bytes, int32_t* tps) {
+  if (!h) return fail(NMPC_E_INVALID, "null handle");
+  if (lds_bytes) *lds_bytes = h->lds_bytes;
+  if (tps) *tps = WAVE;
+  return NMPC_OK;
+}
+
+int nmpc_set_trace(nmpc_handle* h, int32_t enable) {
+  if (!h) return fail(NMPC_E_INVALID, "null handle");
+  h->trace = enable != 0;
+  return NMPC_OK;
+}
+
+int nmpc_read_trace(nmpc_handle* h, int32_t B, double* host_out) {
+  if (!h || !host_out) return fail(NMPC_E_INVALID, "null argument");
+  if (!h->dtrace || B > h->last_B) return fail(NMPC_E_INVALID, "no trace recorded for that batch");
+  const size_t n = (size_t)B * (h->hp.o.max_iter + 1) * TRACE_F;
+  if (hipMemcpy(host_out, h->dtrace, n * sizeof(double), hipMemcpyDeviceToHost) != hipSuccess)
+    return fail(NMPC_E_HIP, "hipMemcpy trace");
+  return NMPC_OK;
+}
+
+int nmpc_solve_batch_dev(nmpc_handle* h, int32_t B, const double* x0, int64_t ld_x0, const double* lbx,
+                         int64_t ld_lbx, const double* ubx, int64_t ld_ubx, const double* lbg, int64_t ld_lbg,
+                         const double* ubg, int64_t ld_ubg, const double* p, int64_t ld_p, double* x_out,
+                         double* f_out, double* g_out, double* lam_x_out, double* lam_g_out, double* X_out,
+                         int32_t* status, int32_t* iters, void* stream) {
+  if (!h) return fail(NMPC_E_INVALID, "null handle");
+  if (B < 0) return fail(NMPC_E_INVALID, "B < 0");
+  if (B == 0) return NMPC_OK;
+  if (!x0 || !lbx || !ubx || !lbg || !ubg || !p || !x_out)
+    return fail(NMPC_E_INVALID, "required pointer is null");
+  const Params& P = h->hp;
+  if ((ld_x0 != 0 && ld_x0 < P.nw) || (ld_lbx != 0 && ld_lbx < P.nw) || (ld_ubx != 0 && ld_ubx < P.nw) ||
+      (ld_lbg != 0 && ld_lbg < P.ng) || (ld_ubg != 0 && ld_ubg < P.ng) || (ld_p != 0 && ld_p < P.np))
+    return fail(NMPC_E_INVALID, "leading dimension smaller than the vector length");
+  IO io;
+  io.x0 = x0; io.lbx = lbx; io.ubx = ubx; io.lbg = lbg; io.ubg = ubg; io.p = p;
+  io.ld_x0 = ld_x0; io.ld_lbx = ld_lbx; io.ld_ubx = ld_ubx; io.ld_lbg = ld_lbg; io.ld_ubg = ld_ubg; io.ld_p = ld_p;
+  io.x_out = x_out; io.f_out = f_out; io.g_out = g_out; io.lam_x = lam_x_out; io.lam_g = lam_g_out;
+  io.X_out = X_out; io.status = status; io.iters = iters; io.trace = nullptr;
+  if (h->trace) {
+    const size_t need = (size_t)B * (P.o.max_iter + 1) * TRACE_F * sizeof(double);
+    if (need > h->trace_bytes) {
+      if (h->dtrace) hipFree(h->dtrace);
+      h->dtrace = nullptr; h->trace_bytes = 0;
+      if (hipMalloc(&h->dtrace, need) != hipSuccess) return fail(NMPC_E_NOMEM, "hipMalloc trace");
+      h->trace_bytes = need;
+    }
+    hipMemsetAsync(h->dtrace, 0, need, (hipStream_t)stream);
+    io.trace = h->dtrace;
+  }
+  h->last_B = B;
+  hipLaunchKernelGGL(nmpc_solve_kernel, dim3(B), dim3(WAVE), h->lds_bytes, (hipStream_t)stream,
+                     (const Params*)h->dprm, (int)B, io);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return fail(NMPC_E_HIP, std::string("kernel launch: ") + hipGetErrorString(e));
+  return NMPC_OK;
+}
+
+int nmpc_solve_batch(nmpc_handle* h, int32_t B, const double* x0, int64_t ld_x0, const double* lbx, int64_t ld_lbx,
+                     const double* ubx, int64_t ld_ubx, const double* lbg, int64_t ld_lbg, const double* ubg,
+                     int64_t ld_ubg, const double* p, int64_t ld_p, double* x_out, double* f_out, double* g_out,
+                     double* lam_x_out, double* lam_g_out, double* X_out, int32_t* status, int32_t* iters) {
+  if (!h) return fail(NMPC_E_INVALID, "null handle");
+  if (B < 0) return fail(NMPC_E_INVALID, "B < 0");
+  if (B == 0) return NMPC_OK;
+  if (!x0 || !lbx || !ubx || !lbg || !ubg || !p || !x_out)
+    return fail(NMPC_E_INVALID, "required pointer is null");
+  const Params& P = h->hp;
+  const size_t nw = P.nw, ng = P.ng, np = P.np, nX = P.nX;
+  auto cols = [&](int64_t ld) { return ld == 0 ? (size_t)1 : (size_t)B; };
+  auto len = [&](int64_t ld, size_t n) { return ld == 0 ? n : (size_t)(B - 1) * (size_t)ld + n; };
+  const size_t n_x0 = len(ld_x0, nw), n_lbx = len(ld_lbx, nw), n_ubx = len(ld_ubx, nw);
+  const size_t n_lbg = len(ld_lbg, ng), n_ubg = len(ld_ubg, ng), n_p = len(ld_p, np);
+  (void)cols;
+  const size_t n_out = (size_t)B * (2 * nw + 2 * ng + nX + 1);
+  const size_t total = n_x0 + n_lbx + n_ubx + n_lbg + n_ubg + n_p + n_out;
+  if (total * sizeof(double) > h->dbuf_bytes) {
+    if (h->dbuf) hipFree(h->dbuf);
+    h->dbuf = nullptr; h->dbuf_bytes = 0;
+    if (hipMalloc(&h->dbuf, total * sizeof(double)) != hipSuccess) return fail(NMPC_E_NOMEM, "hipMalloc staging");
+    h->dbuf_bytes = total * sizeof(double);
+  }
+  if ((size_t)B * 2 * sizeof(int) > h->ibuf_bytes) {
+    if (h->ibuf) hipFree(h->ibuf);
+    h->ibuf = nullptr; h->ibuf_bytes = 0;
+    if (hipMalloc(&h->ibuf, (size_t)B * 2 * sizeof(int)) != hipSuccess) return fail(NMPC_E_NOMEM, "hipMalloc staging");
+    h->ibuf_bytes = (size_t)B * 2 * sizeof(int);
+  }
+  double* q = h->dbuf;
+  double* d_x0 = q; q += n_x0;
+  double* d_lbx = q; q += n_lbx;
+  double* d_ubx = q; q += n_ubx;
+  double* d_lbg = q; q += n_lbg;
+  double* d_ubg = q; q += n_ubg;
+  double* d_p = q; q += n_p;
+  double* d_x = q; q += (size_t)B * nw;
+  double* d_lx = q; q += (size_t)B * nw;
+  double* d_g = q; q += (size_t)B * ng;
+  double* d_lg = q; q += (size_t)B * ng;
+  double* d_X = q; q += (size_t)B * nX;
+  double* d_f = q; q += (size_t)B;
+  int* d_st = h->ibuf;
+  int* d_it = h->ibuf + B;
+  hipError_t e = hipSuccess;
+  auto up = [&](double* dst, const double* src, size_t n) {
+    if (e == hipSuccess) e = hipMemcpy(dst, src, n * sizeof(double), hipMemcpyHostToDevice);
+  };
+  up(d_x0, x0, n_x0); up(d_lbx, lbx, n_lbx); up(d_ubx, ubx, n_ubx);
+  up(d_lbg, lbg, n_lbg); up(d_ubg, ubg, n_ubg); up(d_p, p, n_p);
+  if (e != hipSuccess) return fail(NMPC_E_HIP, std::string("hipMemcpy H2D: ") + hipGetErrorString(e));
+  int rc = nmpc_solve_batch_dev(h, B, d_x0, ld_x0, d_lbx, ld_lbx, d_ubx, ld_ubx, d_lbg, ld_lbg, d_ubg, ld_ubg,
+                                d_p, ld_p, d_x, d_f, d_g, d_lx, d_lg, d_X, d_st, d_it, nullptr);
+  if (rc != NMPC_OK) return rc;
+  e = hipDeviceSynchronize();
+  if (e != hipSuccess) return fail(NMPC_E_HIP, std::string("kernel: ") + hipGetErrorString(e));
+  auto down = [&](void* dst, const void* src, size_t bytes) {
+    if (dst && e == hipSuccess) e = hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost);
+  };
+  down(x_out, d_x, (size_t)B * nw * 8); down(lam_x_out, d_lx, (size_t)B * nw * 8);
+  down(g_out, d_g, (size_t)B * ng * 8); down(lam_g_out, d_lg, (size_t)B * ng * 8);
+  down(X_out, d_X, (size_t)B * nX * 8); down(f_out, d_f, (size_t)B * 8);
+  down(status, d_st, (size_t)B * 4); down(iters, d_it, (size_t)B * 4);
+  if (e != hipSuccess) return fail(NMPC_E_HIP, std::string("hipMemcpy D2H: ") + hipGetErrorString(e));
+  return NMPC_OK;
+}
+
+int nmpc_shift_dev(nmpc_handle* h, int32_t B, double* p, int64_t ld_p, const double* u_sol, double* w_out,
+                   const double* v_t, const double* w_t, void* stream) {
+  if (!h) return fail(NMPC_E_INVALID, "null handle");
+  if (B <= 0) return B == 0 ? NMPC_OK : fail(NMPC_E_INVALID, "B < 0");
+  if (!p || !u_sol || !w_out || !v_t || !w_t) return fail(NMPC_E_INVALID, "null pointer");
+  if (ld_p < h->hp.np) return fail(NMPC_E_INVALID, "ld_p < np");
+  const int thr = 256;
+  hipLaunchKernelGGL(nmpc_shift_kernel, dim3((B + thr - 1) / thr), dim3(thr), 0, (hipStream_t)stream, (int)B,
+                     h->hp.N, h->hp.np, h->hp.T, p, (long long)ld_p, u_sol, w_out, v_t, w_t);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return fail(NMPC_E_HIP, std::string("shift launch: ") + hipGetErrorString(e));
+  return NMPC_OK;
+}
+
+}  // extern "C"

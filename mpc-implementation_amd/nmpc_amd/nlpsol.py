@@ -1,0 +1,246 @@
+"""``nlpsol``-compatible front end over the C-ABI.
+
+Mirrors the reference's operator interface for the hot path:
+
+    solver = ca.nlpsol('solver', 'ipopt', nlp_prob, opts)       Python/NMPC_TT.py:267
+    sol = solver(x0=..., lbx=..., ubx=..., lbg=..., ubg=..., p=...)   :358-365
+    u = ca.reshape(sol['x'], n_controls, N)                     :367
+
+``nlpsol(name, 'ipopt', spec, opts)`` takes a :class:`ProblemSpec` instead of a
+symbolic dict (there is no CasADi here) and the same ``opts`` dict
+(``{'ipopt': {...}, 'print_time': 0}``).  The returned :class:`Solver` is
+called with the same keyword arguments.  Each argument may be one column
+((n,), (n,1)) or a batch of columns ((n,B), CasADi's ``Function.map``
+horzcat convention); bounds given as one column are shared by the batch.
+Results come back as numpy arrays shaped (n,1) for one scenario or (n,B),
+so ``np.reshape(sol['x'], (6, N), order='F')`` is ``ca.reshape``.
+
+Errors follow CasADi: a dimension mismatch raises; non-convergence does not
+(it is reported by ``solver.stats()``, which the reference never reads --
+SURVEY F8).  All arithmetic runs in the HIP library; there is no CPU path.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import Any
+
+import numpy as np
+
+from . import _lib
+from .spec import ProblemSpec
+
+RETURN_STATUS = {
+    0: "Solve_Succeeded", 1: "Solved_To_Acceptable_Level", 2: "Infeasible_Problem_Detected",
+    3: "Search_Direction_Becomes_Too_Small", 4: "Diverging_Iterates",
+    -1: "Maximum_Iterations_Exceeded", -2: "Restoration_Failed", -3: "Error_In_Step_Computation",
+    -11: "Invalid_Problem_Definition", -13: "Invalid_Number_Detected",
+}
+_SUCCESS = (0, 1)
+_DP = C.POINTER(C.c_double)
+_IP = C.POINTER(C.c_int32)
+
+
+def _dptr(a: np.ndarray):
+    return a.ctypes.data_as(_DP)
+
+
+def make_options(opts: dict | None) -> _lib.Options:
+    """IPOPT option dict (CasADi ``opts['ipopt']``) -> C options struct."""
+    o = _lib.default_options()
+    if not opts:
+        return o
+    ip = dict(opts.get("ipopt", {}))
+    for k, v in ip.items():
+        name = _lib.IPOPT_ALIASES.get(k, k)
+        if name in ("print_level", "print_timing_statistics", "sb", "linear_solver", "hessian_approximation",
+                    "mu_strategy", "nlp_scaling_method", "fixed_variable_treatment"):
+            if name == "hessian_approximation" and v != "exact":
+                raise ValueError("only hessian_approximation='exact' is supported")
+            if name == "mu_strategy" and v != "monotone":
+                raise ValueError("only mu_strategy='monotone' (IPOPT default) is supported")
+            if name == "nlp_scaling_method" and v != "gradient-based":
+                raise ValueError("only nlp_scaling_method='gradient-based' (IPOPT default) is supported")
+            continue  # output / linear-solver choices do not change the iterates here
+        if not hasattr(o, name):
+            raise ValueError(f"unsupported IPOPT option {k!r}")
+        setattr(o, name, type(getattr(o, name))(v))
+    for k in opts:
+        if k not in ("ipopt", "print_time", "verbose", "expand", "error_on_fail"):
+            raise ValueError(f"unsupported nlpsol option {k!r}")
+    return o
+
+
+class Solver:
+    """Callable returned by :func:`nlpsol`; one handle (and GPU) per instance."""
+
+    def __init__(self, name: str, spec: ProblemSpec, opts: dict | None = None):
+        spec.validate()
+        self.name = name
+        self.spec = spec
+        self.error_on_fail = bool((opts or {}).get("error_on_fail", False))
+        L = _lib.lib()
+        d = _lib.Desc()
+        d.model = 0
+        d.N, d.np, d.n_obs = spec.N, spec.np, spec.n_obs
+        d.T, d.w1, d.w2, d.vfov, d.hfov = spec.T, spec.w1, spec.w2, spec.vfov, spec.hfov
+        for j, ob in enumerate(spec.obstacles):
+            d.obs_x[j], d.obs_y[j], d.obs_rsum[j] = ob.x, ob.y, ob.r
+            d.obs_x_pidx[j], d.obs_y_pidx[j] = ob.x_pidx, ob.y_pidx
+        d.opts = make_options(opts)
+        self.max_iter = int(d.opts.max_iter)
+        h = C.c_void_p()
+        _lib.check(L.nmpc_create(C.byref(d), C.byref(h)))
+        self._h = h
+        self._stats: dict[str, Any] = {}
+        self.nw, self.ng, self.np, self.nX = spec.nw, spec.ng, spec.np, spec.nX
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            try:
+                _lib.lib().nmpc_destroy(h)
+            except Exception:
+                pass
+            self._h = None
+
+    # ---- argument normalisation (CasADi DM column / matrix semantics)
+    def _arg(self, v, n: int, default: float, name: str):
+        if v is None:
+            return np.full((1, n), default), 0
+        a = np.asarray(v, dtype=np.float64)
+        if a.ndim == 0:
+            a = np.full((n,), float(a))
+        if a.ndim == 1:
+            if a.shape[0] != n:
+                raise ValueError(f"{name}: expected length {n}, got {a.shape[0]}")
+            return np.ascontiguousarray(a.reshape(1, n)), 0
+        if a.ndim == 2:
+            if a.shape[0] != n:
+                raise ValueError(f"{name}: expected {n} rows, got shape {a.shape}")
+            cols = np.ascontiguousarray(a.T)  # (B, n): each scenario contiguous
+            if cols.shape[0] == 1:
+                return cols, 0
+            return cols, n
+        raise ValueError(f"{name}: expected a vector or an (n,B) matrix")
+
+    def __call__(self, x0=None, lbx=None, ubx=None, lbg=None, ubg=None, p=None, **kw):
+        for k in kw:
+            if k not in ("lam_x0", "lam_g0"):
+                raise ValueError(f"unknown argument {k!r}")
+        args = {}
+        B = 1
+        for name, v, n, dflt in (("x0", x0, self.nw, 0.0), ("lbx", lbx, self.nw, -np.inf),
+                                 ("ubx", ubx, self.nw, np.inf), ("lbg", lbg, self.ng, -np.inf),
+                                 ("ubg", ubg, self.ng, np.inf), ("p", p, self.np, 0.0)):
+            a, ld = self._arg(v, n, dflt, name)
+            if ld:
+                if B not in (1, a.shape[0]):
+                    raise ValueError(f"{name}: batch size {a.shape[0]} does not match {B}")
+                B = a.shape[0]
+            args[name] = (a, ld)
+        out = self.solve_batch(B, **{k: v for k, v in args.items()})
+        single = B == 1
+        res = {}
+        for k in ("x", "g", "lam_x", "lam_g", "X"):
+            arr = out[k].T  # (n, B)
+            res[k] = arr if not single else arr.reshape(-1, 1)
+        res["f"] = out["f"].reshape(1, B) if not single else out["f"].reshape(1, 1)
+        res["lam_p"] = np.full((self.np, B) if not single else (self.np, 1), np.nan)  # not computed
+        st = out["status"]
+        self._stats = {
+            "return_status": RETURN_STATUS.get(int(st[0]), str(int(st[0]))) if single
+            else [RETURN_STATUS.get(int(s), str(int(s))) for s in st],
+            "success": bool(st[0] in _SUCCESS) if single else [bool(s in _SUCCESS) for s in st],
+            "iter_count": int(out["iters"][0]) if single else out["iters"].copy(),
+            "status_code": st.copy(),
+        }
+        if self.error_on_fail and not np.all(np.isin(st, _SUCCESS)):
+            raise RuntimeError(f"nlpsol '{self.name}' failed: {self._stats['return_status']}")
+        return res
+
+    def solve_batch(self, B: int, x0, lbx, ubx, lbg, ubg, p):
+        """Arrays as (B or 1, n) C-contiguous + leading dim (0 = broadcast)."""
+        L = _lib.lib()
+        out = {
+            "x": np.empty((B, self.nw)), "g": np.empty((B, self.ng)), "lam_x": np.empty((B, self.nw)),
+            "lam_g": np.empty((B, self.ng)), "X": np.empty((B, self.nX)), "f": np.empty(B),
+            "status": np.empty(B, dtype=np.int32), "iters": np.empty(B, dtype=np.int32),
+        }
+        ins = []
+        for a, ld in (x0, lbx, ubx, lbg, ubg, p):
+            ins += [_dptr(a), ld]
+        _lib.check(L.nmpc_solve_batch(
+            self._h, B, *ins, _dptr(out["x"]), _dptr(out["f"]), _dptr(out["g"]), _dptr(out["lam_x"]),
+            _dptr(out["lam_g"]), _dptr(out["X"]), out["status"].ctypes.data_as(_IP),
+            out["iters"].ctypes.data_as(_IP)))
+        return out
+
+    def solve_device(self, x0, lbx, ubx, lbg, ubg, p, out: dict, stream=None):
+        """Device path: torch CUDA float64 tensors, scenario-major (B, n) or shared (n,).
+
+        ``out`` holds preallocated device tensors x (B,nw) [required], f (B,),
+        g (B,ng), lam_x (B,nw), lam_g (B,ng), X (B,nX), status/iters (B,) int32
+        (optional).  Enqueued on ``stream`` (torch stream; default = current).
+        """
+        import torch  # plumbing only: device memory and streams
+
+        L = _lib.lib()
+        B = out["x"].shape[0]
+
+        def dv(t, n):
+            assert t.dtype == torch.float64 and t.is_cuda and t.is_contiguous()
+            if t.dim() == 1:
+                assert t.shape[0] == n
+                return C.c_void_p(t.data_ptr()), 0
+            assert t.shape == (B, n), (tuple(t.shape), (B, n))
+            return C.c_void_p(t.data_ptr()), n
+
+        ins = []
+        for t, n in ((x0, self.nw), (lbx, self.nw), (ubx, self.nw), (lbg, self.ng), (ubg, self.ng), (p, self.np)):
+            ins += list(dv(t, n))
+
+        def op(k):
+            t = out.get(k)
+            return C.c_void_p(t.data_ptr()) if t is not None else C.c_void_p(0)
+
+        if stream is None:
+            stream = torch.cuda.current_stream()
+        _lib.check(L.nmpc_solve_batch_dev(self._h, B, *ins, op("x"), op("f"), op("g"), op("lam_x"),
+                                          op("lam_g"), op("X"), op("status"), op("iters"),
+                                          C.c_void_p(stream.cuda_stream)))
+
+    def shift_device(self, p, u_sol, w_out, v_t, w_t, stream=None):
+        """Closed-loop shift on device (Python/NMPC_TT.py:13-30), see nmpc_shift_dev."""
+        import torch
+
+        L = _lib.lib()
+        B = u_sol.shape[0]
+        if stream is None:
+            stream = torch.cuda.current_stream()
+        _lib.check(L.nmpc_shift_dev(self._h, B, C.c_void_p(p.data_ptr()), p.shape[1],
+                                    C.c_void_p(u_sol.data_ptr()), C.c_void_p(w_out.data_ptr()),
+                                    C.c_void_p(v_t.data_ptr()), C.c_void_p(w_t.data_ptr()),
+                                    C.c_void_p(stream.cuda_stream)))
+
+    def set_trace(self, enable: bool):
+        _lib.check(_lib.lib().nmpc_set_trace(self._h, int(enable)))
+
+    def read_trace(self, B: int) -> np.ndarray:
+        buf = np.zeros((B, self.max_iter + 1, _lib.TRACE_FIELDS))
+        _lib.check(_lib.lib().nmpc_read_trace(self._h, B, _dptr(buf)))
+        return buf
+
+    def kernel_info(self):
+        lds, tps = C.c_int32(), C.c_int32()
+        _lib.check(_lib.lib().nmpc_kernel_info(self._h, C.byref(lds), C.byref(tps)))
+        return {"lds_bytes": lds.value, "threads_per_scenario": tps.value}
+
+    def stats(self) -> dict:
+        return dict(self._stats)
+
+
+def nlpsol(name: str, plugin: str, spec: ProblemSpec, opts: dict | None = None) -> Solver:
+    """``ca.nlpsol(name, 'ipopt', nlp_prob, opts)`` for the NMPC_TT problem family."""
+    if plugin != "ipopt":
+        raise ValueError(f"only the 'ipopt' plugin is provided (got {plugin!r})")
+    return Solver(name, spec, opts)

@@ -1,0 +1,966 @@
+"""CPU ORACLE -- TEST INFRASTRUCTURE ONLY. NOT PART OF THE PRODUCT.
+
+Only ``tests/``, ``__graft_entry__.smoke()`` and ``bench.py``'s ``cpu_baseline``
+leg may import this module, and only as the *checker*.  The product path
+(``mpc-implementation_amd/``) never imports it and has no CPU fallback.
+
+What this is
+------------
+A plain numpy fp64 restatement of the per-timestep NLP of
+``Python/NMPC_TT.py`` (UAV + 3-DoF gimbal target tracking, FOV cost,
+obstacle-distance constraints) and of the algorithm that solves it there,
+``ca.nlpsol('solver', 'ipopt', ...)`` (``Python/NMPC_TT.py:250-267``).
+
+* Problem functions follow the reference line by line:
+  dynamics ``Python/NMPC_TT.py:139-148``, Euler single-shooting rollout
+  ``:153-167``, FOV/distance objective ``:192-221``, constraint vector
+  ``:234-244`` (10-row layouts: ``Python/10_obstacles.py:272-289``,
+  ``Python/Race Track 2.py:247-264``), bounds ``:269-306`` (generalised to any
+  N / obstacle count), plant/target shift ``:13-30``.
+* Derivatives are hand-derived (chain rule through the ellipse form
+  Q = (r1/a)^2 + (r2/b)^2 of ``:209-220``) and pinned against SymPy goldens
+  (``tests/golden/gen_golden.py``).
+* The solver is a restatement of IPOPT's published primal-dual interior-point
+  filter line-search method (Waechter & Biegler, Math. Prog. 106(1), 2006;
+  IPOPT 3.12/3.14 default options, the version CasADi 3.5.5 -- named in
+  ``MATLAB/Dynamic Obstacles/NMPC_TT.m:2`` -- bundles) applied to the
+  reference's *single-shooting* NLP (decision vector = vec(U) only, F1).
+  Linear algebra is DENSE here: the condensed 6N x 6N primal-dual matrix is
+  assembled explicitly and Cholesky-factorised (inertia test = Cholesky
+  success).  The HIP product computes the same Newton step with a stage-wise
+  Riccati recursion; agreement of the two is the parity test.
+
+Parity status: CasADi/IPOPT is not installed here nor on the GPU box and the
+reference holds no golden vectors, so parity with IPOPT itself is UNPINNED.
+The function layer is pinned by SymPy; converged solutions are cross-checked
+against SciPy's independent SLSQP solver (KKT-point agreement).
+
+Restated IPOPT subset: gradient-based NLP scaling, bound
+relaxation, bound push, least-squares constraint-multiplier initialisation,
+monotone (Fiacco-McCormick) barrier update with fast decrease, inertia
+correction on the Hessian block, fraction-to-boundary, filter line search with
+Armijo/F-type switching, second-order corrections, tiny-step detection,
+kappa_sigma multiplier safeguard, soft restoration phase, optimal/acceptable/
+max-iter termination, honor_original_bounds.  NOT restated: the full
+feasibility-restoration NLP (terminates with status -2 instead) and the
+watchdog procedure.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+
+import numpy as np
+
+PI = math.pi
+EPS = np.finfo(np.float64).eps
+INF = 1e19  # IPOPT nlp_lower/upper_bound_inf: |b| >= 1e19 means "no bound"
+
+# --- reference constants: Python/NMPC_TT.py:57-89, :204-205, :224-231 -------
+V_MIN, V_MAX = 14.0, 30.0
+W2U, W3U, WG = PI / 30, PI / 21, PI / 30
+THETA_U, Z_MIN, Z_MAX = 0.2618, 75.0, 150.0
+PHI_G, THETA_G, SHI_G = PI / 6, PI / 6, PI / 2
+UAV_R = 5.0
+
+# Obstacle layouts (x, y) and obstacle radius.
+OBSTACLE_LAYOUTS = {
+    # Python/NMPC_TT.py:224-231
+    "nmpc_tt": ([(175, 820), (-134, 155), (441, 343)], 30.0),
+    # Python/10_obstacles.py:247-269 (obstacles 4-10 parked at 10000,10000)
+    "10_obstacles": ([(500, 20), (1700, 197), (130, 830)] + [(10000, 10000)] * 7, 100.0),
+    # Python/Race Track 2.py:223-244 (all 10 active)
+    "race_track_2": ([(0, 80), (500, 245), (1000, 70), (1500, 295), (1765, 550),
+                      (1500, 750), (1000, 1005), (500, 800), (-100, 950), (-200, 550)], 50.0),
+    # MATLAB/Dynamic Obstacles/Dynamic Obstacle avoidance.m:98-119 (y of 1-6 are
+    # parameters P(12:17) = p[11:17], :128-133); values here are the initial ys
+    "dynamic": ([(2500, 0), (0, 300), (500, 0), (1000, 300), (1500, 0), (2000, 300),
+                 (1300, 1300), (1300, 1300), (1300, 1300), (1300, 1300)], 50.0),
+}
+
+
+@dataclass
+class Problem:
+    """The reference NLP for one horizon length / obstacle table.
+
+    obs_x_pidx / obs_y_pidx: -1 = constant coordinate, else index into p
+    (dynamic obstacles, MATLAB/Dynamic Obstacles/Dynamic Obstacle avoidance.m:128-133).
+    """
+    N: int = 15
+    T: float = 1.0
+    obs_x: np.ndarray = field(default_factory=lambda: np.zeros(0))
+    obs_y: np.ndarray = field(default_factory=lambda: np.zeros(0))
+    obs_rsum: np.ndarray = field(default_factory=lambda: np.zeros(0))
+    obs_x_pidx: np.ndarray = field(default_factory=lambda: np.zeros(0, dtype=int))
+    obs_y_pidx: np.ndarray = field(default_factory=lambda: np.zeros(0, dtype=int))
+    w1: float = 1.0
+    w2: float = 2.0
+    vfov: float = 1.0
+    hfov: float = 1.0
+    np_: int = 11
+
+    nx = 8
+    nu = 6
+
+    def __post_init__(self):
+        self.obs_x = np.asarray(self.obs_x, dtype=float)
+        self.obs_y = np.asarray(self.obs_y, dtype=float)
+        self.obs_rsum = np.asarray(self.obs_rsum, dtype=float)
+        n = len(self.obs_x)
+        if len(self.obs_x_pidx) != n:
+            self.obs_x_pidx = -np.ones(n, dtype=int)
+        if len(self.obs_y_pidx) != n:
+            self.obs_y_pidx = -np.ones(n, dtype=int)
+        self.obs_x_pidx = np.asarray(self.obs_x_pidx, dtype=int)
+        self.obs_y_pidx = np.asarray(self.obs_y_pidx, dtype=int)
+
+    @property
+    def n_obs(self):
+        return len(self.obs_x)
+
+    @property
+    def m(self):
+        return 5 + self.n_obs
+
+    @property
+    def nw(self):
+        return self.nu * self.N
+
+    @property
+    def ng(self):
+        return self.m * (self.N + 1)
+
+    def obstacles(self, p):
+        ox = self.obs_x.copy()
+        oy = self.obs_y.copy()
+        for j in range(self.n_obs):
+            if self.obs_x_pidx[j] >= 0:
+                ox[j] = p[self.obs_x_pidx[j]]
+            if self.obs_y_pidx[j] >= 0:
+                oy[j] = p[self.obs_y_pidx[j]]
+        return ox, oy
+
+
+def make_problem(layout: str | None, N: int, T: float, dynamic: bool = False) -> Problem:
+    """Problem for a named reference obstacle layout (None = 0 obstacles)."""
+    if layout is None:
+        return Problem(N=N, T=T)
+    xy, r = OBSTACLE_LAYOUTS[layout]
+    ox = np.array([a for a, _ in xy], float)
+    oy = np.array([b for _, b in xy], float)
+    rs = np.full(len(xy), UAV_R + r)
+    ypidx = -np.ones(len(xy), dtype=int)
+    np_ = 11
+    if dynamic:
+        ypidx[:6] = np.arange(11, 17)  # P(12:17) in MATLAB 1-based
+        np_ = 17
+    return Problem(N=N, T=T, obs_x=ox, obs_y=oy, obs_rsum=rs, obs_y_pidx=ypidx, np_=np_)
+
+
+# --- bounds: Python/NMPC_TT.py:269-306, generalised (stride m, N+1 stages) ---
+def bounds(prob: Problem):
+    N, m = prob.N, prob.m
+    lbx = np.tile([V_MIN, -W2U, -W3U, -WG, -WG, -WG], N)
+    ubx = np.tile([V_MAX, W2U, W3U, WG, WG, WG], N)
+    lrow = np.concatenate([[Z_MIN, -THETA_U, -PHI_G, -THETA_G, -SHI_G], np.full(prob.n_obs, -np.inf)])
+    urow = np.concatenate([[Z_MAX, THETA_U, PHI_G, THETA_G, SHI_G], np.zeros(prob.n_obs)])
+    return lbx, ubx, np.tile(lrow, N + 1), np.tile(urow, N + 1)
+
+
+# --- model: Python/NMPC_TT.py:139-148 ----------------------------------------
+def dynamics(x, u):
+    th, ps, v = x[3], x[4], u[0]
+    return np.array([v * math.cos(ps) * math.cos(th), v * math.sin(ps) * math.cos(th),
+                     v * math.sin(th), u[1], u[2], u[3], u[4], u[5]])
+
+
+def unpack_w(prob, w):
+    """w = vec(U), U is nu x N column-major (Python/NMPC_TT.py:247-248)."""
+    return np.asarray(w, float).reshape(prob.N, prob.nu).T
+
+
+def rollout(prob, U, x0):
+    """X[:,0] = P[0:8]; X[:,k+1] = X[:,k] + T f(X[:,k], U[:,k])  (:160-167)."""
+    X = np.zeros((8, prob.N + 1))
+    X[:, 0] = x0
+    for k in range(prob.N):
+        X[:, k + 1] = X[:, k] + prob.T * dynamics(X[:, k], U[:, k])
+    return X
+
+
+def stage_cost(prob, xk, xt, yt):
+    """Literal restatement of Python/NMPC_TT.py:209-220 for one stage."""
+    hv, hh = prob.vfov / 2, prob.hfov / 2
+    z = xk[2]
+    a = (z * math.tan(xk[6] + hv) - z * math.tan(xk[6] - hv)) / 2
+    b = (z * math.tan(xk[5] + hh) - z * math.tan(xk[5] - hh)) / 2
+    c7, s7 = math.cos(xk[7]), math.sin(xk[7])
+    A = c7 ** 2 / a ** 2 + s7 ** 2 / b ** 2
+    B = 2 * c7 * s7 * ((1 / a ** 2) - (1 / b ** 2))
+    C = s7 ** 2 / a ** 2 + c7 ** 2 / b ** 2
+    XE = xk[0] + a + z * math.tan(xk[6] - hv)
+    YE = xk[1] + b + z * math.tan(xk[5] - hh)
+    return (prob.w1 * math.sqrt((xk[0] - xt) ** 2 + (xk[1] - yt) ** 2)
+            + prob.w2 * ((A * (xt - XE) ** 2 + B * (yt - YE) * (xt - XE) + C * (yt - YE) ** 2) - 1))
+
+
+def stage_rows(prob, xk, ox, oy):
+    """g rows for one stage (Python/NMPC_TT.py:234-244)."""
+    d = np.sqrt((xk[0] - ox) ** 2 + (xk[1] - oy) ** 2)
+    return np.concatenate([[xk[2], xk[3], xk[5], xk[6], xk[7]], -d + prob.obs_rsum])
+
+
+def objective(prob, w, p):
+    X = rollout(prob, unpack_w(prob, w), p[:8])
+    return sum(stage_cost(prob, X[:, k], p[8], p[9]) for k in range(prob.N))
+
+
+def constraints(prob, w, p):
+    X = rollout(prob, unpack_w(prob, w), p[:8])
+    ox, oy = prob.obstacles(p)
+    return np.concatenate([stage_rows(prob, X[:, k], ox, oy) for k in range(prob.N + 1)])
+
+
+# --- hand-derived derivatives ------------------------------------------------
+_V = [0, 1, 2, 5, 6, 7]  # state indices the stage cost depends on
+
+
+def stage_cost_derivs(prob, xk, xt, yt):
+    """(value, grad (8,), hess (8,8)) of the stage cost of :209-220.
+
+    Uses the algebraically equal form  Q = A ex^2 + B ex ey + C ey^2
+    = (r1/a)^2 + (r2/b)^2,  r1 = c ex + s ey, r2 = s ex - c ey,
+    ex = xt - XE, ey = yt - YE, XE = x + z*be6, YE = y + z*be5,
+    a = z*al6, b = z*al5, al = (tan(+)-tan(-))/2, be = (tan(+)+tan(-))/2.
+    Local variable order v = (x, y, z, x5, x6, x7).
+    """
+    hv, hh = prob.vfov / 2, prob.hfov / 2
+    x, y, z, x5, x6, x7 = (xk[i] for i in _V)
+    t6p, t6m = math.tan(x6 + hv), math.tan(x6 - hv)
+    t5p, t5m = math.tan(x5 + hh), math.tan(x5 - hh)
+    al6, be6 = (t6p - t6m) / 2, (t6p + t6m) / 2
+    al5, be5 = (t5p - t5m) / 2, (t5p + t5m) / 2
+    al6d, be6d = (t6p ** 2 - t6m ** 2) / 2, (2 + t6p ** 2 + t6m ** 2) / 2
+    al5d, be5d = (t5p ** 2 - t5m ** 2) / 2, (2 + t5p ** 2 + t5m ** 2) / 2
+    s6p, s6m = t6p * (1 + t6p ** 2), t6m * (1 + t6m ** 2)
+    s5p, s5m = t5p * (1 + t5p ** 2), t5m * (1 + t5m ** 2)
+    al6dd, be6dd = s6p - s6m, s6p + s6m
+    al5dd, be5dd = s5p - s5m, s5p + s5m
+
+    ex = xt - x - z * be6
+    ey = yt - y - z * be5
+    gex = np.array([-1.0, 0, -be6, 0, -z * be6d, 0])
+    gey = np.array([0, -1.0, -be5, -z * be5d, 0, 0])
+    Hex = np.zeros((6, 6)); Hex[2, 4] = Hex[4, 2] = -be6d; Hex[4, 4] = -z * be6dd
+    Hey = np.zeros((6, 6)); Hey[2, 3] = Hey[3, 2] = -be5d; Hey[3, 3] = -z * be5dd
+    a = z * al6
+    ga = np.array([0, 0, al6, 0, z * al6d, 0])
+    Ha = np.zeros((6, 6)); Ha[2, 4] = Ha[4, 2] = al6d; Ha[4, 4] = z * al6dd
+    b = z * al5
+    gb = np.array([0, 0, al5, z * al5d, 0, 0])
+    Hb = np.zeros((6, 6)); Hb[2, 3] = Hb[3, 2] = al5d; Hb[3, 3] = z * al5dd
+
+    c, s = math.cos(x7), math.sin(x7)
+    e7 = np.zeros(6); e7[5] = 1.0
+    r1 = c * ex + s * ey
+    r2 = s * ex - c * ey
+    u1 = -s * gex + c * gey
+    u2 = c * gex + s * gey
+    gr1 = c * gex + s * gey - r2 * e7
+    gr2 = s * gex - c * gey + r1 * e7
+    Hr1 = c * Hex + s * Hey + np.outer(e7, u1) + np.outer(u1, e7) - r1 * np.outer(e7, e7)
+    Hr2 = s * Hex - c * Hey + np.outer(e7, u2) + np.outer(u2, e7) - r2 * np.outer(e7, e7)
+
+    e1 = r1 / a
+    ge1 = (gr1 - e1 * ga) / a
+    He1 = (Hr1 - np.outer(ge1, ga) - np.outer(ga, ge1) - e1 * Ha) / a
+    e2 = r2 / b
+    ge2 = (gr2 - e2 * gb) / b
+    He2 = (Hr2 - np.outer(ge2, gb) - np.outer(gb, ge2) - e2 * Hb) / b
+    Q = e1 * e1 + e2 * e2
+    gQ = 2 * (e1 * ge1 + e2 * ge2)
+    HQ = 2 * (np.outer(ge1, ge1) + np.outer(ge2, ge2) + e1 * He1 + e2 * He2)
+
+    dx, dy = x - xt, y - yt
+    d = math.sqrt(dx * dx + dy * dy)
+    gd = np.zeros(6); gd[0], gd[1] = dx / d, dy / d
+    Hd = np.zeros((6, 6))
+    d3 = d ** 3
+    Hd[0, 0], Hd[0, 1], Hd[1, 1] = dy * dy / d3, -dx * dy / d3, dx * dx / d3
+    Hd[1, 0] = Hd[0, 1]
+
+    val = prob.w1 * d + prob.w2 * (Q - 1)
+    g6 = prob.w1 * gd + prob.w2 * gQ
+    H6 = prob.w1 * Hd + prob.w2 * HQ
+    g = np.zeros(8); g[_V] = g6
+    H = np.zeros((8, 8)); H[np.ix_(_V, _V)] = H6
+    return val, g, H
+
+
+def obstacle_derivs(xk, ox, oy):
+    """Row -sqrt((x-ox)^2+(y-oy)^2)+R: gradients (n,2) and Hessians (n,2,2) in (x,y)."""
+    dx, dy = xk[0] - ox, xk[1] - oy
+    d = np.sqrt(dx * dx + dy * dy)
+    G = -np.stack([dx / d, dy / d], axis=1)
+    d3 = d ** 3
+    H = np.zeros((len(ox), 2, 2))
+    H[:, 0, 0] = -dy * dy / d3
+    H[:, 0, 1] = H[:, 1, 0] = dx * dy / d3
+    H[:, 1, 1] = -dx * dx / d3
+    return G, H
+
+
+def dyn_jac(prob, xk, uk):
+    """A = I + T f_x, B = T f_u for the Euler step (:162-167)."""
+    T = prob.T
+    th, ps, v = xk[3], xk[4], uk[0]
+    ct, st, cp, sp = math.cos(th), math.sin(th), math.cos(ps), math.sin(ps)
+    A = np.eye(8)
+    A[0, 3], A[0, 4] = -T * v * cp * st, -T * v * sp * ct
+    A[1, 3], A[1, 4] = -T * v * sp * st, T * v * cp * ct
+    A[2, 3] = T * v * ct
+    B = np.zeros((8, 6))
+    B[0, 0], B[1, 0], B[2, 0] = T * cp * ct, T * sp * ct, T * st
+    for j in range(5):
+        B[3 + j, 1 + j] = T
+    return A, B
+
+
+def dyn_hess(prob, xk, uk, lam):
+    """Second derivatives of lam^T (T f(x,u)): (Hxx (8,8), Hxu (8,6))."""
+    T = prob.T
+    th, ps, v = xk[3], xk[4], uk[0]
+    ct, st, cp, sp = math.cos(th), math.sin(th), math.cos(ps), math.sin(ps)
+    l0, l1, l2 = lam[0], lam[1], lam[2]
+    Hxx = np.zeros((8, 8))
+    Hxx[3, 3] = T * (-l0 * v * cp * ct - l1 * v * sp * ct - l2 * v * st)
+    Hxx[4, 4] = T * (-l0 * v * cp * ct - l1 * v * sp * ct)
+    Hxx[3, 4] = Hxx[4, 3] = T * (l0 * v * sp * st - l1 * v * cp * st)
+    Hxu = np.zeros((8, 6))
+    Hxu[3, 0] = T * (-l0 * cp * st - l1 * sp * st + l2 * ct)
+    Hxu[4, 0] = T * (-l0 * sp * ct + l1 * cp * ct)
+    return Hxx, Hxu
+
+
+class SSEval:
+    """Single-shooting evaluation of the reference NLP at one point w.
+
+    Provides F, grad F, g, J = dg/dw (dense), and the Lagrangian Hessian
+    W = d2/dw2 (obj_factor*F + lam^T g) via the reduced-Hessian identity
+    W = [Z;E]^T H_L [Z;E] with the adjoint multipliers of the Euler dynamics.
+    """
+
+    def __init__(self, prob: Problem, w, p):
+        self.prob = prob
+        N, nw = prob.N, prob.nw
+        self.p = np.asarray(p, float)
+        self.U = unpack_w(prob, w)
+        self.X = rollout(prob, self.U, self.p[:8])
+        self.ox, self.oy = prob.obstacles(self.p)
+        xt, yt = self.p[8], self.p[9]
+        self.F = 0.0
+        self.gl = np.zeros((N + 1, 8))
+        self.Hl = np.zeros((N + 1, 8, 8))
+        for k in range(N):
+            v, g, H = stage_cost_derivs(prob, self.X[:, k], xt, yt)
+            self.F += v
+            self.gl[k], self.Hl[k] = g, H
+        self.g = np.concatenate([stage_rows(prob, self.X[:, k], self.ox, self.oy) for k in range(N + 1)])
+        # dynamics jacobians and forward sensitivities Z_k = dX_k/dw
+        self.A = np.zeros((N, 8, 8))
+        self.B = np.zeros((N, 8, 6))
+        self.Z = np.zeros((N + 1, 8, nw))
+        for k in range(N):
+            self.A[k], self.B[k] = dyn_jac(prob, self.X[:, k], self.U[:, k])
+            self.Z[k + 1] = self.A[k] @ self.Z[k]
+            self.Z[k + 1][:, 6 * k:6 * k + 6] += self.B[k]
+        # constraint-row jacobians wrt X_k
+        m = prob.m
+        self.Gk = np.zeros((N + 1, m, 8))
+        self.Hg = np.zeros((N + 1, prob.n_obs, 2, 2))
+        for k in range(N + 1):
+            for i, idx in enumerate([2, 3, 5, 6, 7]):
+                self.Gk[k, i, idx] = 1.0
+            if prob.n_obs:
+                G2, H2 = obstacle_derivs(self.X[:, k], self.ox, self.oy)
+                self.Gk[k, 5:, 0:2] = G2
+                self.Hg[k] = H2
+        self.gradF = sum(self.Z[k].T @ self.gl[k] for k in range(N))
+        self.J = np.concatenate([self.Gk[k] @ self.Z[k] for k in range(N + 1)], axis=0)
+
+    def hessian(self, obj_factor, lam_g):
+        prob = self.prob
+        N, m, nw = prob.N, prob.m, prob.nw
+        lam = np.asarray(lam_g, float).reshape(N + 1, m)
+        # adjoint: lam_k = obj*gl_k + G_k^T y_k + A_k^T lam_{k+1}
+        adj = np.zeros((N + 2, 8))
+        for k in range(N, 0, -1):
+            adj[k] = obj_factor * self.gl[k] + self.Gk[k].T @ lam[k]
+            if k < N:
+                adj[k] += self.A[k].T @ adj[k + 1]
+        W = np.zeros((nw, nw))
+        for k in range(N + 1):
+            Hxx = obj_factor * self.Hl[k]
+            if prob.n_obs:
+                Hxx[0:2, 0:2] += np.einsum("j,jab->ab", lam[k, 5:], self.Hg[k])
+            Hxu = np.zeros((8, 6))
+            if k < N:
+                dHxx, Hxu = dyn_hess(prob, self.X[:, k], self.U[:, k], adj[k + 1])
+                Hxx = Hxx + dHxx
+            Zk = self.Z[k]
+            W += Zk.T @ Hxx @ Zk
+            if k < N:
+                C = Zk.T @ Hxu  # (nw, 6)
+                W[:, 6 * k:6 * k + 6] += C
+                W[6 * k:6 * k + 6, :] += C.T
+        return W
+
+
+# --- IPOPT restatement --------------------------------------------------------
+IPOPT_DEFAULTS = dict(
+    max_iter=3000, tol=1e-8, acceptable_tol=1e-6, acceptable_iter=15,
+    acceptable_obj_change_tol=1e20, acceptable_dual_inf_tol=1e10,
+    acceptable_constr_viol_tol=1e-2, acceptable_compl_inf_tol=1e-2,
+    dual_inf_tol=1.0, constr_viol_tol=1e-4, compl_inf_tol=1e-4,
+    mu_init=0.1, kappa_mu=0.2, theta_mu=1.5, barrier_tol_factor=10.0, tau_min=0.99,
+    bound_push=1e-2, bound_frac=1e-2, slack_bound_push=1e-2, slack_bound_frac=1e-2,
+    bound_relax_factor=1e-8, bound_mult_init_val=1.0, constr_mult_init_max=1e3,
+    nlp_scaling_max_gradient=100.0, nlp_scaling_min_value=1e-8,
+    kappa_d=1e-5, kappa_sigma=1e10, s_max=100.0,
+    theta_max_fact=1e4, theta_min_fact=1e-4, gamma_theta=1e-5, gamma_phi=1e-8,
+    delta=1.0, s_theta=1.1, s_phi=2.3, eta_phi=1e-8, alpha_red_factor=0.5,
+    alpha_min_frac=0.05, max_soc=4, kappa_soc=0.99, obj_max_inc=5.0,
+    first_hessian_perturbation=1e-4, min_hessian_perturbation=1e-20,
+    max_hessian_perturbation=1e20, perturb_inc_fact_first=100.0,
+    perturb_inc_fact=8.0, perturb_dec_fact=1.0 / 3.0,
+    tiny_step_tol=10 * EPS, soft_resto_pderror_reduction_factor=0.9999,
+    max_soft_resto_iters=10,
+)
+
+# The reference's option dict (Python/NMPC_TT.py:257-265)
+REFERENCE_OPTS = dict(max_iter=100, acceptable_tol=1e-8, acceptable_obj_change_tol=1e-6)
+
+# IPOPT ApplicationReturnStatus codes
+SOLVE_SUCCEEDED, SOLVED_TO_ACCEPTABLE_LEVEL, SEARCH_DIRECTION_TOO_SMALL = 0, 1, 3
+MAXIMUM_ITERATIONS_EXCEEDED, RESTORATION_FAILED, ERROR_IN_STEP_COMPUTATION = -1, -2, -3
+INVALID_NUMBER_DETECTED = -13
+
+
+def _compare_le(lhs, rhs, basval):
+    """IPOPT's Compare_le: lhs <= rhs up to 10*eps*|basval|."""
+    return lhs - rhs <= 10.0 * EPS * abs(basval)
+
+
+class IpoptDense:
+    """Dense restatement of IPOPT on the reference single-shooting NLP."""
+
+    def __init__(self, prob: Problem, opts=None):
+        self.prob = prob
+        o = dict(IPOPT_DEFAULTS)
+        if opts:
+            for k, v in opts.items():
+                if k not in o:
+                    raise KeyError(f"unknown IPOPT option {k}")
+                o[k] = v
+        self.o = o
+
+    # ----- helpers -----------------------------------------------------------
+    def _relax(self, b, sign):
+        o = self.o
+        fin = np.abs(b) < INF
+        r = np.minimum(o["constr_viol_tol"], o["bound_relax_factor"] * np.maximum(1.0, np.abs(b)))
+        out = b.copy()
+        out[fin] = b[fin] + sign * r[fin]
+        return out
+
+    @staticmethod
+    def _push(x, lo, hi, lm, um, kp, kf):
+        """IPOPT DefaultIterateInitializer::push_variables."""
+        x = x.copy()
+        both = lm & um
+        pl = kp * np.maximum(1.0, np.abs(lo))
+        pu = kp * np.maximum(1.0, np.abs(hi))
+        span = np.where(both, hi - lo, np.inf)
+        pl = np.minimum(pl, kf * span)
+        pu = np.minimum(pu, kf * span)
+        x = np.where(lm, np.maximum(x, lo + pl), x)
+        x = np.where(um, np.minimum(x, hi - pu), x)
+        return x
+
+    def _evaluate(self, w):
+        ev = SSEval(self.prob, w, self.p)
+        return ev
+
+    # ----- main entry --------------------------------------------------------
+    def solve(self, x0, lbx, ubx, lbg, ubg, p, trace=False):
+        prob, o = self.prob, self.o
+        n, m = prob.nw, prob.ng
+        self.p = np.asarray(p, float).ravel()
+        lbx, ubx = np.asarray(lbx, float).ravel(), np.asarray(ubx, float).ravel()
+        lbg, ubg = np.asarray(lbg, float).ravel(), np.asarray(ubg, float).ravel()
+        w0 = np.asarray(x0, float).ravel()
+        if np.any((np.abs(lbg) < INF) & (lbg == ubg)):
+            raise ValueError("equality rows (lbg == ubg) are not supported")
+        xlm, xum = lbx > -INF, ubx < INF
+        slm, sum_ = lbg > -INF, ubg < INF
+        xl, xu = self._relax(lbx, -1.0), self._relax(ubx, +1.0)
+        gl_, gu_ = self._relax(lbg, -1.0), self._relax(ubg, +1.0)
+        damp_xl = (xlm & ~xum).astype(float)
+        damp_xu = (xum & ~xlm).astype(float)
+        damp_sl = (slm & ~sum_).astype(float)
+        damp_su = (sum_ & ~slm).astype(float)
+
+        # gradient-based scaling at the user's starting point
+        ev0 = self._evaluate(w0)
+        if not (np.all(np.isfinite(ev0.gradF)) and np.all(np.isfinite(ev0.J))):
+            return self._result(w0, w0, 0, INVALID_NUMBER_DETECTED, 1.0, np.ones(m),
+                                np.zeros(n), np.zeros(n), np.zeros(m), lbx, ubx, [])
+        gmax = np.max(np.abs(ev0.gradF)) if n else 0.0
+        df = 1.0
+        if gmax > o["nlp_scaling_max_gradient"]:
+            df = o["nlp_scaling_max_gradient"] / gmax
+        df = max(df, o["nlp_scaling_min_value"])
+        rowmax = np.max(np.abs(ev0.J), axis=1) if m else np.zeros(0)
+        dc = np.ones(m)
+        if m and np.max(rowmax) > o["nlp_scaling_max_gradient"]:
+            with np.errstate(divide="ignore"):
+                dc = np.minimum(1.0, o["nlp_scaling_max_gradient"] / rowmax)
+            dc = np.maximum(dc, o["nlp_scaling_min_value"])
+        dl, du = dc * gl_, dc * gu_
+        dl = np.where(slm, dl, -np.inf)
+        du = np.where(sum_, du, np.inf)
+
+        # initial point
+        x = self._push(w0, xl, xu, xlm, xum, o["bound_push"], o["bound_frac"])
+        ev = self._evaluate(x)
+        s = self._push(dc * ev.g, dl, du, slm, sum_, o["slack_bound_push"], o["slack_bound_frac"])
+        zl = np.where(xlm, o["bound_mult_init_val"], 0.0)
+        zu = np.where(xum, o["bound_mult_init_val"], 0.0)
+        vl = np.where(slm, o["bound_mult_init_val"], 0.0)
+        vu = np.where(sum_, o["bound_mult_init_val"], 0.0)
+        y = np.zeros(m)
+        if o["constr_mult_init_max"] > 0 and m > 0:
+            J = dc[:, None] * ev.J
+            bx = df * ev.gradF - zl + zu
+            bs = vu - vl
+            wx = np.linalg.solve(np.eye(n) + J.T @ J, bx + J.T @ bs)
+            y = bs - J @ wx
+            if np.max(np.abs(y)) > o["constr_mult_init_max"]:
+                y = np.zeros(m)
+        mu = o["mu_init"]
+        tau = max(o["tau_min"], 1.0 - mu)
+
+        nzx = int(xlm.sum() + xum.sum())
+        nzs = int(slm.sum() + sum_.sum())
+
+        def slacks(x_, s_):
+            return (np.where(xlm, x_ - xl, 1.0), np.where(xum, xu - x_, 1.0),
+                    np.where(slm, s_ - dl, 1.0), np.where(sum_, du - s_, 1.0))
+
+        def barrier_obj(f_, x_, s_, mu_):
+            Sxl, Sxu, Ssl, Ssu = slacks(x_, s_)
+            val = f_
+            val -= mu_ * (np.sum(np.log(Sxl[xlm])) + np.sum(np.log(Sxu[xum]))
+                          + np.sum(np.log(Ssl[slm])) + np.sum(np.log(Ssu[sum_])))
+            val += o["kappa_d"] * mu_ * (np.dot(damp_xl, Sxl * xlm) + np.dot(damp_xu, Sxu * xum)
+                                         + np.dot(damp_sl, Ssl * slm) + np.dot(damp_su, Ssu * sum_))
+            return val
+
+        def grad_lag(gf, J, y_, zl_, zu_, vl_, vu_):
+            return gf + J.T @ y_ - zl_ + zu_, -y_ - vl_ + vu_
+
+        def compl(x_, s_, zl_, zu_, vl_, vu_, mu_):
+            Sxl, Sxu, Ssl, Ssu = slacks(x_, s_)
+            parts = [(Sxl * zl_ - mu_)[xlm], (Sxu * zu_ - mu_)[xum],
+                     (Ssl * vl_ - mu_)[slm], (Ssu * vu_ - mu_)[sum_]]
+            return np.concatenate(parts) if parts else np.zeros(0)
+
+        def err_scaling(y_, zl_, zu_, vl_, vu_):
+            smax = o["s_max"]
+            nd = m + nzx + nzs
+            sd = (np.sum(np.abs(y_)) + np.sum(np.abs(zl_)) + np.sum(np.abs(zu_))
+                  + np.sum(np.abs(vl_)) + np.sum(np.abs(vu_))) / nd if nd else 0.0
+            sd = max(smax, sd) / smax
+            nc = nzx + nzs
+            sc = (np.sum(np.abs(zl_)) + np.sum(np.abs(zu_)) + np.sum(np.abs(vl_)) + np.sum(np.abs(vu_))) / nc if nc else 0.0
+            sc = max(smax, sc) / smax
+            return sd, sc
+
+        def amax(v):
+            return float(np.max(np.abs(v))) if v.size else 0.0
+
+        def frac_to_bound(tau_, x_, s_, dx_, ds_):
+            Sxl, Sxu, Ssl, Ssu = slacks(x_, s_)
+            a = 1.0
+            for S, dS, msk in ((Sxl, dx_, xlm), (Sxu, -dx_, xum), (Ssl, ds_, slm), (Ssu, -ds_, sum_)):
+                sel = msk & (dS < 0)
+                if np.any(sel):
+                    a = min(a, float(np.min(-tau_ * S[sel] / dS[sel])))
+            return a
+
+        def dual_frac_to_bound(tau_, zl_, zu_, vl_, vu_, dzl, dzu, dvl, dvu):
+            a = 1.0
+            for z_, dz_, msk in ((zl_, dzl, xlm), (zu_, dzu, xum), (vl_, dvl, slm), (vu_, dvu, sum_)):
+                sel = msk & (dz_ < 0)
+                if np.any(sel):
+                    a = min(a, float(np.min(-tau_ * z_[sel] / dz_[sel])))
+            return a
+
+        # state of the algorithm
+        f = df * ev.F
+        d = dc * ev.g
+        gf = df * ev.gradF
+        J = dc[:, None] * ev.J
+        filt = []  # list of (phi, theta)
+        theta_max = theta_min = None
+        delta_last, delta_curr = 0.0, 0.0
+        in_soft_resto, soft_resto_counter = False, 0
+        tiny_step_flag = False
+        mu_initialized = False
+        acc_counter = 0
+        last_obj, curr_obj, last_obj_iter = -1e50, -1e50, -1
+        it = 0
+        tr = []
+        status = None
+
+        def nlp_error(x_, s_, d_, gf_, J_, y_, zl_, zu_, vl_, vu_):
+            sd, sc = err_scaling(y_, zl_, zu_, vl_, vu_)
+            glx, gls = grad_lag(gf_, J_, y_, zl_, zu_, vl_, vu_)
+            dinf = max(amax(glx), amax(gls))
+            cviol = amax(np.concatenate([np.maximum(0.0, dl - d_)[slm], np.maximum(0.0, d_ - du)[sum_]]))
+            cmp = amax(compl(x_, s_, zl_, zu_, vl_, vu_, 0.0))
+            return max(dinf / sd, cviol, cmp / sc), dinf, cviol, cmp
+
+        def barrier_error(x_, s_, d_, gf_, J_, y_, zl_, zu_, vl_, vu_, mu_):
+            sd, sc = err_scaling(y_, zl_, zu_, vl_, vu_)
+            glx, gls = grad_lag(gf_, J_, y_, zl_, zu_, vl_, vu_)
+            dinf = max(amax(glx), amax(gls))
+            return max(dinf / sd, amax(d_ - s_), amax(compl(x_, s_, zl_, zu_, vl_, vu_, mu_)) / sc)
+
+        def pd_error(x_, s_, d_, gf_, J_, y_, zl_, zu_, vl_, vu_, mu_):
+            glx, gls = grad_lag(gf_, J_, y_, zl_, zu_, vl_, vu_)
+            dual = (np.sum(np.abs(glx)) + np.sum(np.abs(gls))) / (n + m)
+            prim = np.sum(np.abs(d_ - s_)) / m if m else 0.0
+            nc = nzx + nzs
+            cm = np.sum(np.abs(compl(x_, s_, zl_, zu_, vl_, vu_, mu_))) / nc if nc else 0.0
+            return dual + prim + cm
+
+        while True:
+            # ---------------- convergence check ----------------
+            err, dinf, cviol, cmp = nlp_error(x, s, d, gf, J, y, zl, zu, vl, vu)
+            if not np.isfinite(err):
+                status = INVALID_NUMBER_DETECTED
+                break
+            u_dinf, u_cviol, u_cmp = dinf / df, cviol_unscaled(d, dc, gl_, gu_, slm, sum_), cmp / df
+            if (err <= o["tol"] and u_dinf <= o["dual_inf_tol"] and u_cviol <= o["constr_viol_tol"]
+                    and u_cmp <= o["compl_inf_tol"]):
+                status = SOLVE_SUCCEEDED
+                break
+            if it != last_obj_iter:
+                last_obj, curr_obj, last_obj_iter = curr_obj, f, it
+            acceptable = (err <= o["acceptable_tol"] and u_dinf <= o["acceptable_dual_inf_tol"]
+                          and u_cviol <= o["acceptable_constr_viol_tol"]
+                          and u_cmp <= o["acceptable_compl_inf_tol"]
+                          and abs(curr_obj - last_obj) / max(1.0, abs(curr_obj)) <= o["acceptable_obj_change_tol"])
+            if o["acceptable_iter"] > 0 and acceptable:
+                acc_counter += 1
+                if acc_counter >= o["acceptable_iter"]:
+                    status = SOLVED_TO_ACCEPTABLE_LEVEL
+                    break
+            else:
+                acc_counter = 0
+            if it >= o["max_iter"]:
+                status = MAXIMUM_ITERATIONS_EXCEEDED
+                break
+
+            # ---------------- barrier parameter update ----------------
+            sub_err = barrier_error(x, s, d, gf, J, y, zl, zu, vl, vu, mu)
+            done = False
+            tsf = tiny_step_flag
+            while (sub_err <= o["barrier_tol_factor"] * mu or tsf) and not done:
+                new_mu = min(o["kappa_mu"] * mu, mu ** o["theta_mu"])
+                new_mu = max(new_mu, min(o["tol"], o["compl_inf_tol"]) / (o["barrier_tol_factor"] + 1.0))
+                changed = new_mu != mu
+                if not changed and tsf:
+                    status = SEARCH_DIRECTION_TOO_SMALL
+                    break
+                mu = new_mu
+                tau = max(o["tau_min"], 1.0 - mu)
+                if not changed:
+                    done = True
+                else:
+                    sub_err = barrier_error(x, s, d, gf, J, y, zl, zu, vl, vu, mu)
+                    done = sub_err > o["barrier_tol_factor"] * mu
+                if done and changed:
+                    filt = []
+                    in_soft_resto = False
+                tsf = False
+            if status is not None:
+                break
+            mu_initialized = True
+            tiny_step_flag = False
+
+            # ---------------- search direction ----------------
+            Sxl, Sxu, Ssl, Ssu = slacks(x, s)
+            SigX = np.where(xlm, zl / Sxl, 0.0) + np.where(xum, zu / Sxu, 0.0)
+            SigS = np.where(slm, vl / Ssl, 0.0) + np.where(sum_, vu / Ssu, 0.0)
+            gphi = (gf - np.where(xlm, mu / Sxl, 0.0) + np.where(xum, mu / Sxu, 0.0)
+                    + o["kappa_d"] * mu * (damp_xl - damp_xu))
+            rs = (-y - np.where(slm, mu / Ssl, 0.0) + np.where(sum_, mu / Ssu, 0.0)
+                  + o["kappa_d"] * mu * (damp_sl - damp_su))
+            rd = d - s
+            W = ev.hessian(df, dc * y)
+            if delta_curr > 0:
+                delta_last = delta_curr
+            delta = 0.0
+            fact = None
+            while True:
+                D = SigS + delta
+                M = W + np.diag(SigX + delta) + J.T @ (D[:, None] * J)
+                try:
+                    fact = np.linalg.cholesky(M)
+                    break
+                except np.linalg.LinAlgError:
+                    if delta == 0.0:
+                        delta = (o["first_hessian_perturbation"] if delta_last == 0.0
+                                 else max(o["min_hessian_perturbation"], delta_last * o["perturb_dec_fact"]))
+                    else:
+                        if delta_last == 0.0 or 1e5 * delta_last < delta:
+                            delta *= o["perturb_inc_fact_first"]
+                        else:
+                            delta *= o["perturb_inc_fact"]
+                    if delta > o["max_hessian_perturbation"]:
+                        fact = None
+                        break
+            delta_curr = delta
+            if fact is None:
+                status = ERROR_IN_STEP_COMPUTATION
+                break
+            D = SigS + delta
+
+            def solve_dir(rd_):
+                rhs = -(gphi + J.T @ (y + D * rd_ + rs))
+                t = np.linalg.solve(fact, rhs)
+                dx_ = np.linalg.solve(fact.T, t)
+                ds_ = J @ dx_ + rd_
+                dy_ = D * ds_ + rs
+                dzl_ = np.where(xlm, mu / Sxl - zl - zl / Sxl * dx_, 0.0)
+                dzu_ = np.where(xum, mu / Sxu - zu + zu / Sxu * dx_, 0.0)
+                dvl_ = np.where(slm, mu / Ssl - vl - vl / Ssl * ds_, 0.0)
+                dvu_ = np.where(sum_, mu / Ssu - vu + vu / Ssu * ds_, 0.0)
+                return dx_, ds_, dy_, dzl_, dzu_, dvl_, dvu_
+
+            dx, ds, dy, dzl, dzu, dvl, dvu = solve_dir(rd)
+
+            # ---------------- line search ----------------
+            theta_ref = float(np.sum(np.abs(rd)))
+            phi_ref = barrier_obj(f, x, s, mu)
+            gphi_s = (-np.where(slm, mu / Ssl, 0.0) + np.where(sum_, mu / Ssu, 0.0)
+                      + o["kappa_d"] * mu * (damp_sl - damp_su))
+            gBD = float(np.dot(gphi, dx) + np.dot(gphi_s, ds))
+            if theta_max is None:
+                theta_max = o["theta_max_fact"] * max(1.0, theta_ref)
+                theta_min = o["theta_min_fact"] * max(1.0, theta_ref)
+
+            def is_ftype(a):
+                return gBD < 0.0 and a * (-gBD) ** o["s_phi"] > o["delta"] * theta_ref ** o["s_theta"]
+
+            def armijo(a, phi_t):
+                return _compare_le(phi_t - phi_ref, o["eta_phi"] * a * gBD, phi_ref)
+
+            def acceptable_to_iterate(phi_t, th_t):
+                if phi_t > phi_ref:
+                    basval = 1.0
+                    if abs(phi_ref) > 10.0:
+                        basval = math.log10(abs(phi_ref))
+                    if math.log10(phi_t - phi_ref) > o["obj_max_inc"] + basval:
+                        return False
+                return (_compare_le(th_t, (1.0 - o["gamma_theta"]) * theta_ref, theta_ref)
+                        or _compare_le(phi_t - phi_ref, -o["gamma_phi"] * theta_ref, phi_ref))
+
+            def filter_ok(phi_t, th_t):
+                return all(phi_t <= fp or th_t <= ft for fp, ft in filt)
+
+            def check_accept(a_test, phi_t, th_t):
+                if th_t > theta_max:
+                    return False
+                if a_test > 0.0 and is_ftype(a_test) and theta_ref <= theta_min:
+                    ok = armijo(a_test, phi_t)
+                else:
+                    ok = acceptable_to_iterate(phi_t, th_t)
+                if not ok:
+                    return False
+                return filter_ok(phi_t, th_t)
+
+            def trial(a, dx_, ds_):
+                xt = x + a * dx_
+                st = s + a * ds_
+                evt = self._evaluate(xt)
+                ft = df * evt.F
+                dt = dc * evt.g
+                if not (np.isfinite(ft) and np.all(np.isfinite(dt))):
+                    return None
+                phit = barrier_obj(ft, xt, st, mu)
+                tht = float(np.sum(np.abs(dt - st)))
+                if not np.isfinite(phit):
+                    return None
+                return xt, st, evt, ft, dt, phit, tht
+
+            def try_soft_resto(step):
+                dx_, ds_, dy_, dzl_, dzu_, dvl_, dvu_ = step
+                ap = frac_to_bound(tau, x, s, dx_, ds_)
+                ad = dual_frac_to_bound(tau, zl, zu, vl, vu, dzl_, dzu_, dvl_, dvu_)
+                a = min(ap, ad)
+                tri = trial(a, dx_, ds_)
+                if tri is None:
+                    return None
+                xt, st, evt, ft, dt, phit, tht = tri
+                yt, zlt, zut, vlt, vut = y + a * dy_, zl + a * dzl_, zu + a * dzu_, vl + a * dvl_, vu + a * dvu_
+                gft, Jt = df * evt.gradF, dc[:, None] * evt.J
+                e_t = pd_error(xt, st, dt, gft, Jt, yt, zlt, zut, vlt, vut, mu)
+                e_c = pd_error(x, s, d, gf, J, y, zl, zu, vl, vu, mu)
+                if e_t <= o["soft_resto_pderror_reduction_factor"] * e_c:
+                    orig = check_accept(0.0, phit, tht)
+                    return (a, a, xt, st, evt, ft, dt, yt, zlt, zut, vlt, vut, orig)
+                return None
+
+            accepted = None
+            ls_trials = 0
+            soc_taken = False
+            alpha_p = 0.0
+            alpha_d = 0.0
+            # tiny step detection
+            tiny = (amax(dx / (1.0 + np.abs(x))) <= o["tiny_step_tol"]
+                    and amax(ds / (1.0 + np.abs(s))) <= o["tiny_step_tol"]
+                    and amax(rd) <= 1e-4)
+            step = (dx, ds, dy, dzl, dzu, dvl, dvu)
+            if in_soft_resto:
+                soft_resto_counter += 1
+                if soft_resto_counter <= o["max_soft_resto_iters"]:
+                    r = try_soft_resto(step)
+                    if r is not None:
+                        accepted = ("soft",) + r
+                        if r[-1]:
+                            in_soft_resto = False
+            elif tiny:
+                a = frac_to_bound(tau, x, s, dx, ds)
+                tri = trial(a, dx, ds)
+                if tri is not None:
+                    accepted = ("reg", a, step, tri)
+                    tiny_step_flag = True
+            else:
+                amin = o["gamma_theta"]
+                if gBD < 0:
+                    amin = min(o["gamma_theta"], o["gamma_phi"] * theta_ref / (-gBD))
+                    if theta_ref <= theta_min:
+                        amin = min(amin, o["delta"] * theta_ref ** o["s_theta"] / (-gBD) ** o["s_phi"])
+                amin *= o["alpha_min_frac"]
+                amax_p = frac_to_bound(tau, x, s, dx, ds)
+                a = amax_p
+                n_steps = 0
+                while a > amin or n_steps == 0:
+                    ls_trials += 1
+                    tri = trial(a, dx, ds)
+                    if tri is not None and check_accept(a, tri[5], tri[6]):
+                        accepted = ("reg", a, step, tri)
+                        break
+                    if tri is not None and a == amax_p and theta_ref <= tri[6] and o["max_soc"] > 0:
+                        # second-order correction (FilterLSAcceptor::TrySecondOrderCorrection)
+                        th_tr = tri[6]
+                        th_old = 0.0
+                        a_soc = a
+                        dms = rd.copy()
+                        cnt = 0
+                        cur = tri
+                        while cnt < o["max_soc"] and (cnt == 0 or th_tr <= o["kappa_soc"] * th_old):
+                            th_old = th_tr
+                            dms = a_soc * dms + (cur[4] - cur[1])
+                            stp = solve_dir(dms)
+                            a_soc = frac_to_bound(tau, x, s, stp[0], stp[1])
+                            cur = trial(a_soc, stp[0], stp[1])
+                            if cur is None:
+                                break
+                            if check_accept(a, cur[5], cur[6]):
+                                accepted = ("reg", a_soc, stp, cur)
+                                soc_taken = True
+                                break
+                            cnt += 1
+                            th_tr = cur[6]
+                        if accepted is not None:
+                            break
+                    a *= o["alpha_red_factor"]
+                    n_steps += 1
+                if accepted is None:
+                    r = try_soft_resto(step)
+                    if r is not None:
+                        accepted = ("soft",) + r
+                        if not r[-1]:
+                            in_soft_resto = True
+                            soft_resto_counter = 0
+                elif accepted[0] == "reg":
+                    a_test = a
+                    phi_acc = accepted[3][5]
+                    if not (is_ftype(a_test) and armijo(a_test, phi_acc)):
+                        filt.append((phi_ref - o["gamma_phi"] * theta_ref, (1.0 - o["gamma_theta"]) * theta_ref))
+
+            if accepted is None:
+                status = RESTORATION_FAILED
+                break
+
+            if accepted[0] == "reg":
+                _, alpha_p, stp, tri = accepted
+                x, s, ev, f, d = tri[0], tri[1], tri[2], tri[3], tri[4]
+                alpha_d = dual_frac_to_bound(tau, zl, zu, vl, vu, stp[3], stp[4], stp[5], stp[6])
+                y = y + alpha_p * stp[2]
+                zl, zu = zl + alpha_d * stp[3], zu + alpha_d * stp[4]
+                vl, vu = vl + alpha_d * stp[5], vu + alpha_d * stp[6]
+            else:
+                (_, alpha_p, alpha_d, x, s, ev, f, d, y, zl, zu, vl, vu, _) = accepted
+            # kappa_sigma safeguard (IpoptAlgorithm::correct_bound_multiplier)
+            Sxl, Sxu, Ssl, Ssu = slacks(x, s)
+            ks = o["kappa_sigma"]
+            zl = np.where(xlm, np.maximum(np.minimum(zl, ks * mu / Sxl), mu / (ks * Sxl)), 0.0)
+            zu = np.where(xum, np.maximum(np.minimum(zu, ks * mu / Sxu), mu / (ks * Sxu)), 0.0)
+            vl = np.where(slm, np.maximum(np.minimum(vl, ks * mu / Ssl), mu / (ks * Ssl)), 0.0)
+            vu = np.where(sum_, np.maximum(np.minimum(vu, ks * mu / Ssu), mu / (ks * Ssu)), 0.0)
+            gf = df * ev.gradF
+            J = dc[:, None] * ev.J
+            it += 1
+            if trace:
+                tr.append(dict(iter=it, mu=mu, f=f, theta=float(np.sum(np.abs(d - s))), delta=delta_curr,
+                               alpha_p=alpha_p, alpha_d=alpha_d, ls=ls_trials, soc=soc_taken))
+
+        return self._result(x, w0, it, status, df, dc, zl, zu, y, lbx, ubx, tr, mu=mu)
+
+    def _result(self, x, w0, it, status, df, dc, zl, zu, y, lbx, ubx, tr, mu=None):
+        prob = self.prob
+        xf = np.minimum(np.maximum(x, lbx), ubx)  # honor_original_bounds
+        ev = SSEval(prob, xf, self.p)
+        X = ev.X
+        return dict(x=xf, f=ev.F, g=ev.g, lam_x=(zu - zl) / df, lam_g=y * dc / df,
+                    X=X, status=status, iter=it, trace=tr, df=df, dc=dc, mu=mu)
+
+
+def cviol_unscaled(d, dc, gl_, gu_, slm, sum_):
+    """Unscaled constraint violation (max norm) w.r.t. the relaxed bounds."""
+    g = d / dc
+    v = np.concatenate([np.maximum(0.0, gl_ - g)[slm], np.maximum(0.0, g - gu_)[sum_]])
+    return float(np.max(v)) if v.size else 0.0
+
+
+# --- closed loop (immediate caller, Python/NMPC_TT.py:13-30, :346-402) --------
+def shift_timestep(prob, x0, u, xs, con_t=(12.0, 0.01)):
+    """Plant Euler step with u[:,0], warm start shift, target unicycle step."""
+    T = prob.T
+    x0n = x0 + T * dynamics(x0, u[:, 0])
+    u0 = np.concatenate([u[:, 1:], u[:, -1:]], axis=1)
+    v, w = con_t
+    xsn = xs + T * np.array([v * math.cos(xs[2]), v * math.sin(xs[2]), w])
+    return x0n, u0, xsn
+
+
+def fov_centre(x0, vfov=1.0, hfov=1.0):
+    """FOV centre of the current state (Python/NMPC_TT.py:397-400)."""
+    a_p = (x0[2] * math.tan(x0[6] + vfov / 2) - x0[2] * math.tan(x0[6] - vfov / 2)) / 2
+    b_p = (x0[2] * math.tan(x0[5] + hfov / 2) - x0[2] * math.tan(x0[5] - hfov / 2)) / 2
+    return x0[0] + a_p + x0[2] * math.tan(x0[6] - vfov / 2), x0[1] + b_p + x0[2] * math.tan(x0[5] - hfov / 2)
