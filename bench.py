@@ -1,0 +1,194 @@
+"""Benchmark: batched NMPC steps/s on MI355X (BASELINE.json metric).
+
+One *step* = one batched MPC step over B scenarios per GPU: every scenario's
+per-timestep NLP (Python/NMPC_TT.py:358-365) solved by the HIP kernel,
+warm-started from the previous step's shifted solution, followed by the
+closed-loop shift on device (Python/NMPC_TT.py:13-30) and, for N>1 GPUs, the
+RCCL gather of each scenario's applied control and status to rank 0.
+
+Workload (config 3 of BASELINE.json / SURVEY.md section 8): 4096 scenarios
+per GPU, N=20, 10 static obstacles (Python/Race Track 2.py layout), T=0.2,
+fp64, the reference's IPOPT options (max_iter=100, tol 1e-8).  Weak scaling:
+per-GPU batch fixed as the GPU count grows.
+
+Prints ONE JSON line on rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "mpc-implementation_amd"))
+
+FP64_PEAK_TFLOPS = 78.6      # MI355X FP64 vector = FP64 matrix peak (AMD spec)
+HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md chip table
+KFLOP_PER_STAGE_ITER = 7.5   # ~6.2k Riccati + ~1k assembly per stage-iteration
+
+
+def survey_bytes_per_step(spec, ibar):
+    """SURVEY.md 8(d) streamed-KKT byte model (fp64)."""
+    nx, nu, m, N = 8, 6, spec.m, spec.N
+    s_stage = 8 * ((nx + nu) ** 2 + nx * (nx + nu) + m * nx + 3 * (nx + nu) + 2 * nx + 4 * m + 4 * nu
+                   + nx * nx + nu * nx + nu * nu + nx + nu)
+    b_iter = 2 * (N + 1) * s_stage
+    io = 8 * ((spec.np + spec.nw) + (spec.nw + 8 * (N + 1) + 2))
+    return ibar * b_iter + io, s_stage, b_iter, io
+
+
+def cpu_baseline(spec_cfg, P, lbx, ubx, lbg, ubg, budget_s=15.0):
+    """Time the CPU oracle (numpy dense IPOPT restatement, 1 core) on a bounded
+    sample of the same scenarios (cold start)."""
+    sys.path.insert(0, ROOT)
+    from oracle import nmpc_oracle as orc
+
+    layout = "race_track_2" if spec_cfg.n_obs == 10 else (None if spec_cfg.n_obs == 0 else "nmpc_tt")
+    prob = orc.make_problem(layout, N=spec_cfg.N, T=spec_cfg.T)
+    solver = orc.IpoptDense(prob, orc.REFERENCE_OPTS)
+    t0 = time.perf_counter()
+    n = 0
+    iters = 0
+    while n < P.shape[0] and (time.perf_counter() - t0) < budget_s:
+        r = solver.solve(np.zeros(spec_cfg.nw), lbx, ubx, lbg, ubg, P[n])
+        iters += r["iter"]
+        n += 1
+    el = time.perf_counter() - t0
+    return {"value": n / el, "unit": "MPC steps/s", "cores": 1, "kind": "port",
+            "sample": f"{n} cold-start solves of the first {n} config-3 scenarios by "
+                      f"oracle/nmpc_oracle.py (numpy, dense single-shooting IPOPT restatement) "
+                      f"in {el:.1f}s, mean {iters / max(n, 1):.1f} iterations"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--batch", type=int, default=4096, help="scenarios per GPU")
+    ap.add_argument("--config", type=int, default=3)
+    ap.add_argument("--mode", choices=["closed_loop", "cold"], default="closed_loop")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-budget", type=float, default=15.0)
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+    from nmpc_amd import nlpsol, config_spec, draw_scenarios, REFERENCE_OPTS
+    from nmpc_amd.dist import shard, pack_result, gather_rows
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    dev = torch.device("cuda", local_rank if world > 1 else 0)
+
+    spec = config_spec(args.config)
+    B = args.batch
+    # global scenario stream, sliced per rank (results independent of world size)
+    P_all = draw_scenarios(spec, B * world, seed=1000 + args.config)
+    P = P_all[shard(B * world, world, rank)]
+    lbx, ubx, lbg, ubg = spec.bounds()
+    solver = nlpsol("solver", "ipopt", spec, REFERENCE_OPTS)
+
+    f64 = dict(dtype=torch.float64, device=dev)
+    t_lbx, t_ubx = torch.tensor(lbx, **f64), torch.tensor(ubx, **f64)
+    t_lbg, t_ubg = torch.tensor(lbg, **f64), torch.tensor(ubg, **f64)
+    p = torch.tensor(P, **f64).contiguous()
+    w = torch.zeros(B, spec.nw, **f64)
+    out = {"x": torch.empty(B, spec.nw, **f64), "f": torch.empty(B, **f64),
+           "status": torch.empty(B, dtype=torch.int32, device=dev),
+           "iters": torch.empty(B, dtype=torch.int32, device=dev)}
+    v_t = torch.full((B,), 12.0, **f64)   # target speed, Python/NMPC_TT.py:25
+    w_t = torch.full((B,), 0.01, **f64)   # target turn rate
+    stream = torch.cuda.current_stream()
+
+    iters_sum = torch.zeros((), dtype=torch.int64, device=dev)
+    ok_sum = torch.zeros((), dtype=torch.int64, device=dev)
+    status_hist = {}
+
+    def one_step(timed_events=None):
+        if timed_events is not None:
+            timed_events[0].record(stream)
+        solver.solve_device(w if args.mode == "closed_loop" else torch.zeros_like(w),
+                            t_lbx, t_ubx, t_lbg, t_ubg, p, out, stream=stream)
+        if timed_events is not None:
+            timed_events[1].record(stream)
+        if args.mode == "closed_loop":
+            solver.shift_device(p, out["x"], w, v_t, w_t, stream=stream)
+        if world > 1:  # the only exchange: per-step gather of (u0, f, status) to every rank
+            gather_rows(pack_result(out["x"], out["f"], out["status"]), world)
+
+    for _ in range(args.warmup):
+        one_step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    st_list = []
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        one_step(evs[k])
+        iters_sum += out["iters"].sum()
+        st_list.append(out["status"].clone())
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    kern_ms = [a.elapsed_time(b) for a, b in evs]
+    el_t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    tot = torch.stack([iters_sum.double(), torch.tensor(float(B * args.steps), **f64)])
+    if world > 1:
+        dist.all_reduce(el_t, op=dist.ReduceOp.MAX)
+        dist.all_reduce(tot, op=dist.ReduceOp.SUM)
+    elapsed = float(el_t.item())
+    ibar = float(tot[0].item() / tot[1].item())
+    sts = torch.cat(st_list).cpu().numpy()
+    for s_ in np.unique(sts):
+        status_hist[int(s_)] = int((sts == s_).sum())
+
+    if rank == 0:
+        total_steps = B * world * args.steps
+        value = total_steps / elapsed
+        ms_per_step = elapsed / args.steps * 1e3
+        kern_avg_s = float(np.mean(kern_ms)) / 1e3
+        flops_launch = B * ibar * (spec.N + 1) * KFLOP_PER_STAGE_ITER * 1e3
+        achieved = flops_launch / kern_avg_s / 1e12
+        bps, s_stage, b_iter, io = survey_bytes_per_step(spec, ibar)
+        res = {
+            "metric": "MPC steps/sec (batched scenarios), N=20 UAV+gimbal, 10 obstacles",
+            "value": value, "unit": "MPC steps/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
+            "config": {"workload": f"config {args.config}: batch={B}/GPU, N={spec.N}, {spec.n_obs} static "
+                                   f"obstacles (Race Track 2.py), T={spec.T}, reference IPOPT opts, "
+                                   f"{args.mode.replace('_', '-')} warm-started MPC steps",
+                       "global_batch": B * world, "seq_len": spec.N, "parallelism": f"dp{world}"},
+            "roofline": {"bound": "mfma", "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                         "frac": achieved / FP64_PEAK_TFLOPS, "traffic": None,
+                         "kernel": "nmpc_solve_kernel", "kernel_avg_ms": kern_avg_s * 1e3,
+                         "model": f"SURVEY 8(d) {KFLOP_PER_STAGE_ITER} kflop/stage-iteration x (N+1) x "
+                                  f"I_bar={ibar:.2f} x B per launch; FP64 peak (vector = matrix)"},
+            "survey_hbm_model": {"bytes_per_step": bps, "S_stage": s_stage, "B_iter": b_iter, "IO": io,
+                                 "equivalent_GBs": B * bps / kern_avg_s / 1e9,
+                                 "io_only_GBs": B * io / kern_avg_s / 1e9},
+            "mean_ip_iterations": ibar,
+            "status_histogram": status_hist,
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            res["cpu_baseline"] = cpu_baseline(spec, P, lbx, ubx, lbg, ubg, budget_s=args.cpu_budget)
+        print(json.dumps(res))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

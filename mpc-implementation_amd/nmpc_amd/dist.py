@@ -1,0 +1,38 @@
+"""Multi-GPU sharding of independent scenarios.
+
+Scenarios are independent NLPs: each rank (one process per GPU) solves a
+contiguous block of the global scenario stream with no data-path collective.
+The only exchange is the per-step gather of each scenario's applied control,
+cost and status (8 doubles = 64 B per scenario) so that every rank -- in
+particular the controller on rank 0 -- holds the whole batch's result.  Over
+RCCL (backend "nccl") this is one all-gather of B*64 bytes per rank.
+"""
+from __future__ import annotations
+
+
+def shard(total: int, world: int, rank: int) -> slice:
+    """Contiguous block of the global scenario index range for `rank`."""
+    base, rem = divmod(total, world)
+    lo = rank * base + min(rank, rem)
+    return slice(lo, lo + base + (1 if rank < rem else 0))
+
+
+def pack_result(x, f, status):
+    """(B, 8) float64 rows: u0 (first control column), f, status."""
+    import torch
+
+    return torch.cat([x[:, :6], f[:, None], status[:, None].to(x.dtype)], dim=1).contiguous()
+
+
+def gather_rows(local, world: int, group=None):
+    """All-gather equal-sized (B, k) row blocks from every rank -> (world*B, k)."""
+    import torch
+    import torch.distributed as dist
+
+    out = torch.empty((world * local.shape[0],) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
+    if dist.get_backend(group) == "nccl":
+        dist.all_gather_into_tensor(out, local, group=group)
+    else:  # gloo (CPU tests)
+        parts = list(out.chunk(world))
+        dist.all_gather(parts, local, group=group)
+    return out

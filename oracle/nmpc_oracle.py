@@ -385,8 +385,11 @@ class SSEval:
                 G2, H2 = obstacle_derivs(self.X[:, k], self.ox, self.oy)
                 self.Gk[k, 5:, 0:2] = G2
                 self.Hg[k] = H2
-        self.gradF = sum(self.Z[k].T @ self.gl[k] for k in range(N))
-        self.J = np.concatenate([self.Gk[k] @ self.Z[k] for k in range(N + 1)], axis=0)
+        # stage 0 is constant in w (X_0 = p[0:8], F7): Z_0 = 0, so its terms are
+        # structurally absent -- as in CasADi's symbolic AD -- and are skipped
+        # rather than multiplied by zero (a 0*NaN would poison the result).
+        self.gradF = sum((self.Z[k].T @ self.gl[k] for k in range(1, N)), np.zeros(nw))
+        self.J = np.concatenate([np.zeros((m, nw))] + [self.Gk[k] @ self.Z[k] for k in range(1, N + 1)], axis=0)
 
     def hessian(self, obj_factor, lam_g):
         prob = self.prob
@@ -399,7 +402,7 @@ class SSEval:
             if k < N:
                 adj[k] += self.A[k].T @ adj[k + 1]
         W = np.zeros((nw, nw))
-        for k in range(N + 1):
+        for k in range(1, N + 1):
             Hxx = obj_factor * self.Hl[k]
             if prob.n_obs:
                 Hxx[0:2, 0:2] += np.einsum("j,jab->ab", lam[k, 5:], self.Hg[k])

@@ -1,0 +1,282 @@
+"""GPU parity tests: the HIP solver (through the C-ABI) against the CPU oracle
+(oracle/nmpc_oracle.py, dense single-shooting IPOPT restatement) and the
+committed golden solutions.
+
+Tolerance (BASELINE.json north star): trajectories within 1e-6 relative
+error, |a-b| <= 1e-6 (1+|b|), for scenarios both solvers converge on.  In
+practice the two agree iteration for iteration (same status, same iteration
+count, ~1e-14 differences), which is also asserted where it is robust.
+"""
+import glob
+import os
+
+import numpy as np
+import pytest
+
+from oracle import nmpc_oracle as orc
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+TOL = 1e-6
+
+
+def _rel(a, b):
+    return float(np.max(np.abs(np.asarray(a) - np.asarray(b)) / (1.0 + np.abs(np.asarray(b)))))
+
+
+def _solver(spec, opts=None, **kw):
+    from nmpc_amd import nlpsol, REFERENCE_OPTS
+
+    return nlpsol("solver", "ipopt", spec, REFERENCE_OPTS if opts is None else opts)
+
+
+def _oracle(layout, N, T, dynamic=False):
+    prob = orc.make_problem(layout, N=N, T=T, dynamic=dynamic)
+    return prob, orc.IpoptDense(prob, orc.REFERENCE_OPTS)
+
+
+@pytest.mark.parametrize("layout,N,T,B,seed", [
+    ("race_track_2", 20, 0.2, 4, 1003),   # config 3 family
+    (None, 20, 0.2, 3, 1002),             # config 2 family (no obstacles)
+    ("nmpc_tt", 15, 1.0, 2, 1001),        # Python/NMPC_TT.py as written (T=1, NLP scaling active)
+    ("10_obstacles", 15, 0.2, 3, 1004),   # Python/10_obstacles.py layout
+    ("race_track_2", 8, 0.2, 3, 7),
+])
+def test_parity_with_oracle(layout, N, T, B, seed):
+    from nmpc_amd import make_spec, draw_scenarios
+
+    spec = make_spec(layout, N=N, T=T)
+    P = draw_scenarios(spec, B, seed=seed)
+    lbx, ubx, lbg, ubg = spec.bounds()
+    s = _solver(spec)
+    sol = s(x0=np.zeros(spec.nw), lbx=lbx, ubx=ubx, lbg=lbg, ubg=ubg, p=P.T)
+    st = s.stats()
+    prob, ref = _oracle(layout, N, T)
+    for b in range(B):
+        r = ref.solve(np.zeros(spec.nw), lbx, ubx, lbg, ubg, P[b])
+        assert st["status_code"][b] == r["status"], (b, st["status_code"][b], r["status"])
+        assert abs(int(st["iter_count"][b]) - r["iter"]) <= 2
+        if r["status"] == 0:
+            assert _rel(sol["x"][:, b], r["x"]) <= TOL
+            assert _rel(sol["X"][:, b], r["X"].T.ravel()) <= TOL
+            assert _rel(sol["f"][0, b], r["f"]) <= TOL
+            assert _rel(sol["g"][:, b], r["g"]) <= TOL
+
+
+def test_iteration_traces_match_oracle():
+    from nmpc_amd import make_spec, draw_scenarios
+
+    spec = make_spec("race_track_2", N=20, T=0.2)
+    P = draw_scenarios(spec, 2, seed=1003)
+    lbx, ubx, lbg, ubg = spec.bounds()
+    s = _solver(spec)
+    s.set_trace(True)
+    s(x0=np.zeros(spec.nw), lbx=lbx, ubx=ubx, lbg=lbg, ubg=ubg, p=P.T)
+    tr = s.read_trace(2)
+    _, ref = _oracle("race_track_2", 20, 0.2)
+    for b in range(2):
+        r = ref.solve(np.zeros(spec.nw), lbx, ubx, lbg, ubg, P[b], trace=True)
+        for k in range(min(8, len(r["trace"]))):
+            o = r["trace"][k]
+            g = tr[b, k]
+            assert g[1] == pytest.approx(o["mu"], rel=1e-12)
+            assert g[2] == pytest.approx(o["f"], rel=1e-10)
+            assert g[5] == pytest.approx(o["alpha_p"], rel=1e-8, abs=1e-12)
+            assert g[7] == o["ls"]
+
+
+@pytest.mark.parametrize("path", sorted(glob.glob(os.path.join(GOLD, "solutions_*.npz"))))
+def test_golden_solutions(path):
+    from nmpc_amd import make_spec
+
+    z = np.load(path)
+    spec = make_spec(str(z["layout"]), N=int(z["N"]), T=float(z["T"]))
+    lbx, ubx, lbg, ubg = spec.bounds()
+    s = _solver(spec)
+    sol = s(x0=np.zeros(spec.nw), lbx=lbx, ubx=ubx, lbg=lbg, ubg=ubg, p=z["p"].T)
+    st = s.stats()
+    for b in range(len(z["p"])):
+        assert st["status_code"][b] == z["status"][b]
+        if z["status"][b] == 0:
+            assert _rel(sol["x"][:, b], z["x"][b]) <= TOL
+            assert _rel(sol["f"][0, b], z["f"][b]) <= TOL
+            assert _rel(sol["lam_g"][:, b], z["lam_g"][b]) <= 1e-4
+
+
+def test_dynamic_obstacles_parity():
+    from nmpc_amd import make_spec, draw_scenarios
+
+    spec = make_spec("dynamic", N=12, T=0.2, dynamic=True)
+    P = draw_scenarios(spec, 3, seed=1005)
+    lbx, ubx, lbg, ubg = spec.bounds()
+    s = _solver(spec)
+    sol = s(x0=np.zeros(spec.nw), lbx=lbx, ubx=ubx, lbg=lbg, ubg=ubg, p=P.T)
+    _, ref = _oracle("dynamic", 12, 0.2, dynamic=True)
+    for b in range(3):
+        r = ref.solve(np.zeros(spec.nw), lbx, ubx, lbg, ubg, P[b])
+        assert s.stats()["status_code"][b] == r["status"]
+        if r["status"] == 0:
+            assert _rel(sol["x"][:, b], r["x"]) <= TOL
+
+
+def test_single_scenario_shapes_and_broadcast_bounds():
+    from nmpc_amd import make_spec, draw_scenarios
+
+    spec = make_spec("race_track_2", N=10, T=0.2)
+    P = draw_scenarios(spec, 3, seed=5)
+    lbx, ubx, lbg, ubg = spec.bounds()
+    s = _solver(spec)
+    one = s(x0=np.zeros((spec.nw, 1)), lbx=lbx[:, None], ubx=ubx[:, None], lbg=lbg, ubg=ubg, p=P[1][:, None])
+    assert one["x"].shape == (spec.nw, 1) and one["f"].shape == (1, 1) and one["g"].shape == (spec.ng, 1)
+    assert isinstance(s.stats()["return_status"], str)
+    u = np.reshape(one["x"], (6, spec.N), order="F")  # ca.reshape(sol['x'], 6, N)
+    assert u.shape == (6, spec.N)
+    # per-scenario (batched) bounds give bitwise the same result as broadcast bounds
+    rep = lambda v: np.repeat(v[:, None], 3, axis=1)
+    a = s(x0=np.zeros(spec.nw), lbx=lbx, ubx=ubx, lbg=lbg, ubg=ubg, p=P.T)
+    b = s(x0=np.zeros((spec.nw, 3)), lbx=rep(lbx), ubx=rep(ubx), lbg=rep(lbg), ubg=rep(ubg), p=P.T)
+    np.testing.assert_array_equal(a["x"], b["x"])
+    np.testing.assert_array_equal(a["x"][:, 1:2], one["x"])
+    with pytest.raises(ValueError):
+        s(x0=np.zeros(spec.nw + 1), lbx=lbx, ubx=ubx, lbg=lbg, ubg=ubg, p=P[0])
+
+
+def test_invalid_inputs_reported_per_scenario():
+    from nmpc_amd import make_spec, draw_scenarios
+
+    spec = make_spec("race_track_2", N=6, T=0.2)
+    P = draw_scenarios(spec, 4, seed=8)
+    lbx, ubx, lbg, ubg = spec.bounds()
+    LB = np.repeat(lbx[:, None], 4, 1); UB = np.repeat(ubx[:, None], 4, 1)
+    LG = np.repeat(lbg[:, None], 4, 1); UG = np.repeat(ubg[:, None], 4, 1)
+    Pt = P.T.copy()
+    LB[3, 0] = UB[3, 0] + 1.0          # lbx > ubx -> Invalid_Problem_Definition
+    LG[0, 1] = UG[0, 1] = 100.0        # equality row (unsupported) -> Invalid_Problem_Definition
+    Pt[2, 2] = np.nan                  # NaN in p -> Invalid_Number_Detected
+    s = _solver(spec)
+    s(x0=np.zeros(spec.nw), lbx=LB, ubx=UB, lbg=LG, ubg=UG, p=Pt)
+    sc = s.stats()["status_code"]
+    assert sc[0] == -11 and sc[1] == -11
+    assert sc[2] == -13
+    assert sc[3] in (0, 1)             # untouched scenario unaffected by its neighbours
+
+
+def test_empty_batch_is_noop():
+    import ctypes as C
+    from nmpc_amd import _lib, make_spec
+
+    s = _solver(make_spec(None, N=4, T=0.2))
+    assert _lib.lib().nmpc_solve_batch(s._h, 0, *([None, 0] * 6), *([None] * 6), None, None) == 0
+
+
+@pytest.mark.parametrize("N,layout", [(1, "race_track_2"), (63, None)])
+def test_horizon_limits(N, layout):
+    from nmpc_amd import make_spec, draw_scenarios
+
+    spec = make_spec(layout, N=N, T=0.2)
+    P = draw_scenarios(spec, 1, seed=3)
+    lbx, ubx, lbg, ubg = spec.bounds()
+    s = _solver(spec)
+    sol = s(x0=np.zeros(spec.nw), lbx=lbx, ubx=ubx, lbg=lbg, ubg=ubg, p=P.T)
+    _, ref = _oracle(layout, N, 0.2)
+    r = ref.solve(np.zeros(spec.nw), lbx, ubx, lbg, ubg, P[0])
+    assert s.stats()["status_code"][0] == r["status"]
+    if r["status"] == 0:
+        assert _rel(sol["x"][:, 0], r["x"]) <= TOL
+
+
+def test_max_obstacles_and_infinite_bounds():
+    from nmpc_amd import spec as S
+    from nmpc_amd import draw_scenarios
+
+    rng = np.random.default_rng(0)
+    obs = tuple(S.Obstacle(float(x), float(y), 40.0) for x, y in rng.uniform(-300, 1500, (16, 2)))
+    spec = S.ProblemSpec(N=10, T=0.2, obstacles=obs).validate()
+    P = draw_scenarios(spec, 2, seed=4)
+    lbx, ubx, lbg, ubg = spec.bounds()
+    lbx = lbx.copy(); ubg = ubg.copy()
+    lbx[1::6] = -np.inf                 # no lower bound on omega_2u
+    ubg[5::spec.m] = np.inf             # first obstacle row free
+    s = _solver(spec)
+    sol = s(x0=np.zeros(spec.nw), lbx=lbx, ubx=ubx, lbg=lbg, ubg=ubg, p=P.T)
+    prob = orc.Problem(N=10, T=0.2, obs_x=[o.x for o in obs], obs_y=[o.y for o in obs],
+                       obs_rsum=[o.r for o in obs])
+    ref = orc.IpoptDense(prob, orc.REFERENCE_OPTS)
+    for b in range(2):
+        r = ref.solve(np.zeros(spec.nw), lbx, ubx, lbg, ubg, P[b])
+        assert s.stats()["status_code"][b] == r["status"]
+        if r["status"] == 0:
+            assert _rel(sol["x"][:, b], r["x"]) <= TOL
+
+
+def test_full_size_properties():
+    """BASELINE config 3 at full size (4096 scenarios): determinism,
+    batch-position invariance, KKT certificate on a sample, status set."""
+    from nmpc_amd import config_spec, draw_scenarios
+
+    spec = config_spec(3)
+    B = 4096
+    P = draw_scenarios(spec, B, seed=1003)
+    lbx, ubx, lbg, ubg = spec.bounds()
+    s = _solver(spec)
+    a = s(x0=np.zeros(spec.nw), lbx=lbx, ubx=ubx, lbg=lbg, ubg=ubg, p=P.T)
+    sa = s.stats()["status_code"].copy()
+    b = s(x0=np.zeros(spec.nw), lbx=lbx, ubx=ubx, lbg=lbg, ubg=ubg, p=P.T)
+    np.testing.assert_array_equal(a["x"], b["x"])
+    assert set(np.unique(sa)) <= {0, 1, -1, -2, 3}
+    assert np.mean(sa == 0) > 0.95
+    one = s(x0=np.zeros(spec.nw), lbx=lbx, ubx=ubx, lbg=lbg, ubg=ubg, p=P[1234])
+    np.testing.assert_array_equal(one["x"][:, 0], a["x"][:, 1234])
+    prob = orc.make_problem("race_track_2", N=spec.N, T=spec.T)
+    idx = np.flatnonzero(sa == 0)[:: max(1, int(np.sum(sa == 0)) // 16)][:16]
+    for i in idx:
+        ev = orc.SSEval(prob, a["x"][:, i], P[i])
+        stat = ev.gradF + ev.J.T @ a["lam_g"][:, i] + a["lam_x"][:, i]
+        assert np.max(np.abs(stat)) <= 1e-6 * (1 + np.max(np.abs(ev.gradF)))
+        assert np.all(ev.g <= ubg + 1e-6) and np.all(ev.g >= lbg - 1e-6)
+
+
+def test_device_path_matches_host_path():
+    import torch
+    from nmpc_amd import make_spec, draw_scenarios
+
+    spec = make_spec("race_track_2", N=20, T=0.2)
+    B = 8
+    P = draw_scenarios(spec, B, seed=11)
+    lbx, ubx, lbg, ubg = spec.bounds()
+    s = _solver(spec)
+    h = s(x0=np.zeros(spec.nw), lbx=lbx, ubx=ubx, lbg=lbg, ubg=ubg, p=P.T)
+    f64 = dict(dtype=torch.float64, device="cuda")
+    out = {"x": torch.empty(B, spec.nw, **f64), "f": torch.empty(B, **f64),
+           "status": torch.empty(B, dtype=torch.int32, device="cuda"),
+           "iters": torch.empty(B, dtype=torch.int32, device="cuda")}
+    s.solve_device(torch.zeros(B, spec.nw, **f64), torch.tensor(lbx, **f64), torch.tensor(ubx, **f64),
+                   torch.tensor(lbg, **f64), torch.tensor(ubg, **f64), torch.tensor(P, **f64), out)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(out["x"].cpu().numpy(), h["x"].T)
+    np.testing.assert_array_equal(out["status"].cpu().numpy(), s.stats()["status_code"])
+
+
+def test_shift_kernel_matches_reference_shift():
+    import torch
+    from nmpc_amd import make_spec, draw_scenarios
+
+    spec = make_spec("race_track_2", N=20, T=0.2)
+    B = 5
+    P = draw_scenarios(spec, B, seed=12)
+    rng = np.random.default_rng(1)
+    lbx, ubx, _, _ = spec.bounds()
+    U = rng.uniform(lbx, ubx, (B, spec.nw))
+    s = _solver(spec)
+    f64 = dict(dtype=torch.float64, device="cuda")
+    p = torch.tensor(P, **f64)
+    w = torch.empty(B, spec.nw, **f64)
+    s.shift_device(p, torch.tensor(U, **f64), w, torch.full((B,), 12.0, **f64), torch.full((B,), 0.01, **f64))
+    torch.cuda.synchronize()
+    prob = orc.make_problem("race_track_2", N=20, T=0.2)
+    for b in range(B):
+        u = U[b].reshape(spec.N, 6).T
+        x1, u1, xs1 = orc.shift_timestep(prob, P[b, :8], u, P[b, 8:11])
+        np.testing.assert_allclose(p[b, :8].cpu().numpy(), x1, rtol=1e-15, atol=1e-12)
+        np.testing.assert_allclose(p[b, 8:11].cpu().numpy(), xs1, rtol=1e-15, atol=1e-12)
+        np.testing.assert_array_equal(w[b].cpu().numpy(), u1.T.ravel())
