@@ -41,6 +41,25 @@ def survey_bytes_per_step(spec, ibar):
     return ibar * b_iter + io, s_stage, b_iter, io
 
 
+def pmc_traffic():
+    """HBM bytes per solve launch from the newest committed rocprofv3 PMC pass
+    (profiles/r*_pmc_fetch_write.csv): FETCH_SIZE is doubled per the gfx950
+    correction (MI355X_MICROARCH.md, HBM section), WRITE_SIZE taken as is; KB -> B."""
+    import csv
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_fetch_write.csv")))
+    if not files:
+        return None, None
+    fetch, write = [], []
+    for row in csv.DictReader(open(files[-1])):
+        if "nmpc_solve_kernel" not in row.get("Kernel_Name", ""):
+            continue
+        (fetch if row["Counter_Name"] == "FETCH_SIZE" else write).append(float(row["Counter_Value"]))
+    if not fetch or not write:
+        return None, None
+    return (2.0 * np.mean(fetch) + np.mean(write)) * 1024.0, os.path.relpath(files[-1], ROOT)
+
+
 def cpu_baseline(spec_cfg, P, lbx, ubx, lbg, ubg, budget_s=15.0):
     """Time the CPU oracle (numpy dense IPOPT restatement, 1 core) on a bounded
     sample of the same scenarios (cold start)."""
@@ -163,6 +182,7 @@ def main():
         flops_launch = B * ibar * (spec.N + 1) * KFLOP_PER_STAGE_ITER * 1e3
         achieved = flops_launch / kern_avg_s / 1e12
         bps, s_stage, b_iter, io = survey_bytes_per_step(spec, ibar)
+        traffic, traffic_src = pmc_traffic()
         res = {
             "metric": "MPC steps/sec (batched scenarios), N=20 UAV+gimbal, 10 obstacles",
             "value": value, "unit": "MPC steps/s", "n_gpus": world, "steps": args.steps,
@@ -173,7 +193,9 @@ def main():
                                    f"{args.mode.replace('_', '-')} warm-started MPC steps",
                        "global_batch": B * world, "seq_len": spec.N, "parallelism": f"dp{world}"},
             "roofline": {"bound": "mfma", "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
-                         "frac": achieved / FP64_PEAK_TFLOPS, "traffic": None,
+                         "frac": achieved / FP64_PEAK_TFLOPS, "traffic": traffic,
+                         "traffic_unit": "HBM bytes per launch (2*FETCH_SIZE + WRITE_SIZE)",
+                         "traffic_source": traffic_src,
                          "kernel": "nmpc_solve_kernel", "kernel_avg_ms": kern_avg_s * 1e3,
                          "model": f"SURVEY 8(d) {KFLOP_PER_STAGE_ITER} kflop/stage-iteration x (N+1) x "
                                   f"I_bar={ibar:.2f} x B per launch; FP64 peak (vector = matrix)"},
