@@ -102,6 +102,20 @@ __device__ __forceinline__ int boxidx(int i) {  // g rows 0..4: z, theta, x5, x6
 
 enum SumMode { SUM_NEWTON = 0, SUM_LS = 1, SUM_SOC = 2 };
 
+// Diagnostic phase timers (-DNMPC_STAMPS builds only): shader-clock cycles per
+// phase, accumulated by lane 0 in LDS and written to the two spare rows of the
+// trace buffer.  Never compiled into the product library.
+enum Phase { PH_ROLLOUT, PH_EVAL, PH_DERIVS, PH_ADJ, PH_SUMM, PH_RIC, PH_RESOLVE, PH_FWD, PH_ROWSTEP,
+             PH_BARR, PH_FTB, PH_DFTB, PH_CONV, PH_ACCEPT, PH_INIT, PH_TOTAL, PH_COUNT };
+#ifdef NMPC_STAMPS
+#define STAMP0() const unsigned long long _ts0 = __builtin_amdgcn_s_memtime()
+#define STAMP1(ph) do { const unsigned long long _ts1 = __builtin_amdgcn_s_memtime(); \
+    if (lane == 0) stamps[ph] += (double)(_ts1 - _ts0); } while (0)
+#else
+#define STAMP0() do {} while (0)
+#define STAMP1(ph) do {} while (0)
+#endif
+
 struct Solver {
   const Params* __restrict__ P;
   double* sm;
@@ -114,7 +128,7 @@ struct Solver {
   double *s, *y, *vl, *vu, *d, *dt, *ds, *ds2, *dc, *dl, *du, *dms;
   double *gl, *Hl, *trig, *st, *lam;
   double *K, *kf, *Lc, *Pa, *Pb, *pva, *pvb, *PA, *BtP, *St;
-  double *pp, *obx, *oby, *inc, *filt;
+  double *pp, *obx, *oby, *inc, *filt, *stamps;
   // uniform scalars
   double df, mu, tau, delta;
   int nfilt;
@@ -137,6 +151,7 @@ struct Solver {
     PA = sm + prm->PA; BtP = sm + prm->BtP; St = sm + prm->St;
     pp = sm + prm->p; obx = sm + prm->ob; oby = obx + NMPC_MAX_OBS; inc = sm + prm->inc;
     filt = sm + prm->filt;
+    stamps = sm + prm->red;
   }
 
   __device__ __forceinline__ bool hasl(double v) const { return v > -INFINITY; }
@@ -147,6 +162,7 @@ struct Solver {
   // Each lane k sums the increments j<k in order, i.e. bitwise the sequential
   // recursion; the (x,y,z) increments need theta_j, psi_j, so two passes.
   __device__ void rollout(const double* Us, double* Xd) {
+    STAMP0();
     const int k = lane;
     if (k < N) {
 #pragma unroll
@@ -182,6 +198,7 @@ struct Solver {
 #pragma unroll
       for (int c = 0; c < 5; ++c) xk[3 + c] = a[c];
     }
+    STAMP1(PH_ROLLOUT);
     sync();
   }
 
@@ -216,6 +233,7 @@ struct Solver {
 
   // f = sum_k l_k(X) and rows dst[r] = dc[r] * g_r(X) (dc may be null -> unscaled)
   __device__ double eval_fg(const double* Xs, double* dst, const double* scale) {
+    STAMP0();
     const int k = lane;
     double f = 0.0;
     if (k <= N) {
@@ -228,13 +246,16 @@ struct Solver {
       }
     }
     sync();
-    return wsum(f);
+    const double fs = wsum(f);
+    STAMP1(PH_EVAL);
+    return fs;
   }
 
   // --------------------------------------------- stage derivatives at X (lane=k)
   // gl[k] = grad l_k (8), Hl[k] = hess l_k packed over (x,y,z,x5,x6,x7), trig[k].
   // Derivation: oracle/nmpc_oracle.py::stage_cost_derivs (Q = (r1/a)^2+(r2/b)^2).
   __device__ void derivs(const double* Xs, const double* Us) {
+    STAMP0();
     const int k = lane;
     if (k <= N) {
       const double* xk = Xs + k * 8;
@@ -319,6 +340,7 @@ struct Solver {
         }
       }
     }
+    STAMP1(PH_DERIVS);
     sync();
   }
 
@@ -338,6 +360,7 @@ struct Solver {
   // lam_N = G_N^T y_N; lam_k = ofac*gl_k + G_k^T y_k + A_k^T lam_{k+1}
   // (oracle SSEval.hessian).  yy may be null (objective only).
   __device__ void adjoint(double ofac, const double* yy) {
+    STAMP0();
     const int k = lane;
     double* wv = inc;  // scratch 8*(N+1)
     if (k <= N) {
@@ -386,6 +409,7 @@ struct Solver {
       lam[k * 8 + 3] = a3;
       lam[k * 8 + 4] = a4;
     }
+    STAMP1(PH_ADJ);
     sync();
   }
 
@@ -408,6 +432,7 @@ struct Solver {
   // barrier objective phi (oracle barrier_obj) at (u, s + a*ds) [sv == null -> s]
   __device__ double barrier_obj(double f, const double* u, const double* sb, const double* dsv,
                                 double a) const {
+    STAMP0();
     double logs = 0.0, damp = 0.0;
     for (int i = lane; i < nw; i += WAVE) {
       const bool lo = hasl(xl[i]), hi = hasu(xu[i]);
@@ -426,7 +451,9 @@ struct Solver {
     }
     logs = wsum(logs);
     damp = wsum(damp);
-    return f - mu * logs + P->o.kappa_d * mu * damp;
+    const double rr = f - mu * logs + P->o.kappa_d * mu * damp;
+    STAMP1(PH_BARR);
+    return rr;
   }
 
   // -------------------------------------------- Riccati: per-stage summaries
@@ -436,6 +463,7 @@ struct Solver {
   //  SOC:    q only, with rd := dms
   //  LS:     Q += Gt^T Gt ; q += -Gt^T (vu - vl)           (least-squares y init)
   __device__ void summaries(int mode) {
+    STAMP0();
     const int k = lane;
     if (k <= N) {
       const double* xk = X + k * 8;
@@ -483,6 +511,7 @@ struct Solver {
       for (int i = 0; i < 5; ++i) { o16[3 + i] = Qb[i]; o16[10 + i] = qb[i]; }
       o16[8] = qx; o16[9] = qy;
     }
+    STAMP1(PH_SUMM);
     sync();
   }
 
@@ -536,6 +565,12 @@ struct Solver {
   //   hfac, gfac: factors on the stage cost Hessian / gradient; dyn: add the
   //   dynamics second derivatives; Rd: diag of R (null -> 1).
   __device__ bool riccati(double hfac, double gfac, bool dyn, const double* Rd, const double* rv) {
+    STAMP0();
+    const bool r = riccati_(hfac, gfac, dyn, Rd, rv);
+    STAMP1(PH_RIC);
+    return r;
+  }
+  __device__ bool riccati_(double hfac, double gfac, bool dyn, const double* Rd, const double* rv) {
     const int i = lane >> 3, j = lane & 7;
     double* Pc = Pa;
     double* Pn = Pb;
@@ -684,6 +719,7 @@ struct Solver {
 
   // gradient-only re-solve with the stored factors (second-order correction)
   __device__ void resolve(double gfac, const double* rv) {
+    STAMP0();
     // every lane runs the vector recursion redundantly (no LDS exchange)
     double p8[8];
 #pragma unroll
@@ -728,12 +764,14 @@ struct Solver {
 #pragma unroll
       for (int i = 0; i < 8; ++i) p8[i] = pn[i];
     }
+    STAMP1(PH_RESOLVE);
     sync();
   }
 
   // forward sweep: du_k = K_k dx_k + k_k ; dx_{k+1} = A_k dx_k + B_k du_k
   // (redundant in every lane, broadcast LDS reads; lane 0 stores)
   __device__ void forward(double* dUo, double* dXo) {
+    STAMP0();
     double dx[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) dx[i] = 0.0;
@@ -764,11 +802,13 @@ struct Solver {
 #pragma unroll
       for (int c = 0; c < 8; ++c) dx[c] = xn[c];
     }
+    STAMP1(PH_FWD);
     sync();
   }
 
   // ds_r = Gt_r dX_k + rd_r (J dU = G Z dU = G dX)
   __device__ void row_step(const double* dXs, const double* rdsrc, bool rd_is_dms, double* dso) {
+    STAMP0();
     for (int r = lane; r < ng; r += WAVE) {
       const int k = r / m, i = r - k * m;
       const double* xk = X + k * 8;
@@ -785,11 +825,13 @@ struct Solver {
       const double rd = rd_is_dms ? rdsrc[r] : d[r] - s[r];
       dso[r] = jd + rd;
     }
+    STAMP1(PH_ROWSTEP);
     sync();
   }
 
   // primal fraction to the boundary (oracle frac_to_bound)
   __device__ double frac_to_bound(double tau_, const double* dUs, const double* dss) const {
+    STAMP0();
     double a = 1.0;
     for (int i = lane; i < nw; i += WAVE) {
       const double dx = dUs[i];
@@ -801,7 +843,9 @@ struct Solver {
       if (hasl(dl[r]) && dd < 0) a = fmin(a, (-tau_ * (s[r] - dl[r])) / dd);
       if (hasu(du[r]) && -dd < 0) a = fmin(a, (-tau_ * (du[r] - s[r])) / (-dd));
     }
-    return wmin(a);
+    a = wmin(a);
+    STAMP1(PH_FTB);
+    return a;
   }
 
   // dual step components (oracle solve_dir) -- current slacks
@@ -816,6 +860,7 @@ struct Solver {
     if (hasu(du[r])) { const double S = du[r] - s[r]; dvu = mu / S - vu[r] + vu[r] / S * dsv; }
   }
   __device__ double dual_frac_to_bound(double tau_, const double* dUs, const double* dss) const {
+    STAMP0();
     double a = 1.0;
     for (int i = lane; i < nw; i += WAVE) {
       double a1, a2;
@@ -829,7 +874,9 @@ struct Solver {
       if (hasl(dl[r]) && a1 < 0) a = fmin(a, (-tau_ * vl[r]) / a1);
       if (hasu(du[r]) && a2 < 0) a = fmin(a, (-tau_ * vu[r]) / a2);
     }
-    return wmin(a);
+    a = wmin(a);
+    STAMP1(PH_DFTB);
+    return a;
   }
 
   // rs_r (oracle rs) and D_r
@@ -916,10 +963,14 @@ __global__ __launch_bounds__(WAVE) void nmpc_solve_kernel(const Params* __restri
   const int lane = threadIdx.x;
   Solver S;
   S.bind(prm, smem, lane, b);
+  double* stamps = S.stamps;
+  if (lane < PH_COUNT) stamps[lane] = 0.0;
+  const unsigned long long _tk0 = __builtin_amdgcn_s_memtime();
+  (void)_tk0;
   const nmpc_options& o = prm->o;
   const int N = S.N, nw = S.nw, ng = S.ng, m = S.m;
   const int max_iter = o.max_iter;
-  double* trace = io.trace ? io.trace + (long long)b * (max_iter + 1) * TRACE_F : nullptr;
+  double* trace = io.trace ? io.trace + (long long)b * (max_iter + 2) * TRACE_F : nullptr;
 
   // ---------------- load scenario data
   for (int i = lane; i < prm->np; i += WAVE) S.pp[i] = io.p[(long long)b * io.ld_p + i];
@@ -1096,6 +1147,9 @@ __global__ __launch_bounds__(WAVE) void nmpc_solve_kernel(const Params* __restri
     }
   }
 
+#ifdef NMPC_STAMPS
+  if (lane == 0) stamps[PH_INIT] += (double)(__builtin_amdgcn_s_memtime() - _tk0);
+#endif
   // ---------------- main loop
   double f = 0.0;
   if (status == 0) {
@@ -1114,6 +1168,7 @@ __global__ __launch_bounds__(WAVE) void nmpc_solve_kernel(const Params* __restri
   while (running) {
     // ===== adjoint with current y (grad of the Lagrangian, Hessian multipliers)
     S.adjoint(S.df, S.y);
+    STAMP0();
     // ===== optimality error (IpoptCalculatedQuantities::curr_nlp_error)
     double dinf = 0, cviol = 0, ucviol = 0, cmp = 0, sumy = 0, sumz = 0, sumv = 0, pinf = 0;
     bool bad = false;
@@ -1194,6 +1249,7 @@ __global__ __launch_bounds__(WAVE) void nmpc_solve_kernel(const Params* __restri
       tiny_flag = false;
     }
     const double mu = S.mu, tau = S.tau;
+    STAMP1(PH_CONV);
 
     // ===== search direction with inertia correction (PDPerturbationHandler)
     for (int i = lane; i < nw; i += WAVE) {
@@ -1441,6 +1497,7 @@ __global__ __launch_bounds__(WAVE) void nmpc_solve_kernel(const Params* __restri
 
     // ===== accept the trial point (IpoptAlgorithm::AcceptTrialPoint)
     {
+      STAMP0();
       const double* dUa = (acc_kind == 2) ? S.dU2 : S.dU;
       const double* dsa = (acc_kind == 2) ? S.ds2 : S.ds;
       if (acc_kind != 3) alpha_d = S.dual_frac_to_bound(tau, dUa, dsa);
@@ -1481,6 +1538,7 @@ __global__ __launch_bounds__(WAVE) void nmpc_solve_kernel(const Params* __restri
       }
       sync();
       f = f_acc;
+      STAMP1(PH_ACCEPT);
       if (!derivs_done) S.derivs(S.X, S.U);
       else {
         // soft resto computed derivatives at the trial; trig uses U (same values)
@@ -1518,6 +1576,14 @@ __global__ __launch_bounds__(WAVE) void nmpc_solve_kernel(const Params* __restri
     const int nX = prm->nX;
     for (int i = lane; i < nX; i += WAVE) io.X_out[(long long)b * nX + i] = S.Xt[i];
   }
+#ifdef NMPC_STAMPS
+  if (trace) {
+    sync();
+    if (lane == 0) stamps[PH_TOTAL] = (double)(__builtin_amdgcn_s_memtime() - _tk0);
+    sync();
+    if (lane < PH_COUNT) trace[(long long)max_iter * TRACE_F + lane] = stamps[lane];
+  }
+#endif
   if (lane == 0) {
     if (io.f_out) io.f_out[b] = fo;
     if (io.status) io.status[b] = status;
@@ -1695,7 +1761,7 @@ int nmpc_set_trace(nmpc_handle* h, int32_t enable) {
 int nmpc_read_trace(nmpc_handle* h, int32_t B, double* host_out) {
   if (!h || !host_out) return fail(NMPC_E_INVALID, "null argument");
   if (!h->dtrace || B > h->last_B) return fail(NMPC_E_INVALID, "no trace recorded for that batch");
-  const size_t n = (size_t)B * (h->hp.o.max_iter + 1) * TRACE_F;
+  const size_t n = (size_t)B * (h->hp.o.max_iter + 2) * TRACE_F;
   if (hipMemcpy(host_out, h->dtrace, n * sizeof(double), hipMemcpyDeviceToHost) != hipSuccess)
     return fail(NMPC_E_HIP, "hipMemcpy trace");
   return NMPC_OK;
@@ -1721,7 +1787,7 @@ int nmpc_solve_batch_dev(nmpc_handle* h, int32_t B, const double* x0, int64_t ld
   io.x_out = x_out; io.f_out = f_out; io.g_out = g_out; io.lam_x = lam_x_out; io.lam_g = lam_g_out;
   io.X_out = X_out; io.status = status; io.iters = iters; io.trace = nullptr;
   if (h->trace) {
-    const size_t need = (size_t)B * (P.o.max_iter + 1) * TRACE_F * sizeof(double);
+    const size_t need = (size_t)B * (P.o.max_iter + 2) * TRACE_F * sizeof(double);
     if (need > h->trace_bytes) {
       if (h->dtrace) hipFree(h->dtrace);
       h->dtrace = nullptr; h->trace_bytes = 0;

@@ -15,6 +15,9 @@ TRACE_FIELDS = 8
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libnmpc_amd.so")
+# diagnostics only: NMPC_LIB=<path> loads e.g. the -DNMPC_STAMPS phase-timer build
+if os.environ.get("NMPC_LIB"):
+    LIB_PATH = os.environ["NMPC_LIB"]
 
 # every symbol include/nmpc_amd.h declares (checked by tests/test_capi.py)
 EXPORTS = (
