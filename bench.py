@@ -128,11 +128,13 @@ def main():
     w_t = torch.full((B,), 0.01, **f64)   # target turn rate
     stream = torch.cuda.current_stream()
 
-    iters_sum = torch.zeros((), dtype=torch.int64, device=dev)
-    ok_sum = torch.zeros((), dtype=torch.int64, device=dev)
     status_hist = {}
 
-    def one_step(timed_events=None):
+    iters_hist = torch.zeros(max(args.steps, args.warmup), B, dtype=torch.int32, device=dev)
+    st_hist = torch.zeros(max(args.steps, args.warmup), B, dtype=torch.int32, device=dev)
+
+    def one_step(k, timed_events=None):
+        # identical work in warmup and timed steps (torch kernels load lazily on first use)
         if timed_events is not None:
             timed_events[0].record(stream)
         solver.solve_device(w if args.mode == "closed_loop" else torch.zeros_like(w),
@@ -143,20 +145,19 @@ def main():
             solver.shift_device(p, out["x"], w, v_t, w_t, stream=stream)
         if world > 1:  # the only exchange: per-step gather of (u0, f, status) to every rank
             gather_rows(pack_result(out["x"], out["f"], out["status"]), world)
+        iters_hist[k].copy_(out["iters"])
+        st_hist[k].copy_(out["status"])
 
-    for _ in range(args.warmup):
-        one_step()
+    for k in range(args.warmup):
+        one_step(k)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
-    st_list = []
     t0 = time.perf_counter()
     for k in range(args.steps):
-        one_step(evs[k])
-        iters_sum += out["iters"].sum()
-        st_list.append(out["status"].clone())
+        one_step(k, evs[k])
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -164,13 +165,14 @@ def main():
     elapsed = time.perf_counter() - t0
     kern_ms = [a.elapsed_time(b) for a, b in evs]
     el_t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    iters_sum = iters_hist[:args.steps].sum()
     tot = torch.stack([iters_sum.double(), torch.tensor(float(B * args.steps), **f64)])
     if world > 1:
         dist.all_reduce(el_t, op=dist.ReduceOp.MAX)
         dist.all_reduce(tot, op=dist.ReduceOp.SUM)
     elapsed = float(el_t.item())
     ibar = float(tot[0].item() / tot[1].item())
-    sts = torch.cat(st_list).cpu().numpy()
+    sts = st_hist[:args.steps].cpu().numpy()
     for s_ in np.unique(sts):
         status_hist[int(s_)] = int((sts == s_).sum())
 

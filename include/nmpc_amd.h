@@ -135,7 +135,7 @@ int nmpc_solve_batch_dev(nmpc_handle* h, int32_t B,
  * solve records NMPC_TRACE_FIELDS doubles per iteration per scenario
  * {iter, mu, f_scaled, theta, delta_w, alpha_pr, alpha_du, ls_trials}
  * into a device buffer readable with nmpc_read_trace (host pointer,
- * B x (max_iter+2) x NMPC_TRACE_FIELDS, row-major; the last two rows of each
+ * B x (max_iter+3) x NMPC_TRACE_FIELDS, row-major; the last three rows of each
  * scenario are reserved for diagnostic phase timers). */
 #define NMPC_TRACE_FIELDS 8
 int nmpc_set_trace(nmpc_handle* h, int32_t enable);

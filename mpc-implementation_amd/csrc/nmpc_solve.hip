@@ -36,6 +36,8 @@
 namespace {
 
 constexpr int WAVE = 64;
+#define LDS __attribute__((address_space(3)))
+#define CST __attribute__((address_space(4)))
 constexpr double BIGB = 1e19;  // IPOPT nlp_{lower,upper}_bound_inf
 constexpr int FCAP = 128;      // filter capacity (>= max_iter of the reference opts)
 constexpr int TRACE_F = NMPC_TRACE_FIELDS;
@@ -56,7 +58,7 @@ struct Params {
   int X, Xt, dX, dX2;
   int s, y, vl, vu, d, dt, ds, ds2, dc, dl, du, dms;
   int gl, Hl, trig, st, lam;
-  int K, kf, Lc, P0, P1, pv0, pv1, PA, BtP, St;
+  int K, kf, Lc, P0, P1, pv0, pv1, PA, BtP, St, Rt;
   int p, ob, inc, filt, red;
   int total;
 };
@@ -85,6 +87,24 @@ __device__ __forceinline__ double wmin(double v) {
   return v;
 }
 __device__ __forceinline__ bool wany(bool b) { return __any((int)b) != 0; }
+// reciprocal / reciprocal square root: hardware estimate + two Newton steps
+// (~1 ulp; the IEEE-exact fp64 division sequence is ~2x longer).  Only used on
+// finite non-zero arguments (slacks, distances, pivots).
+__device__ __forceinline__ double rcp(double x) {
+  double y = __builtin_amdgcn_rcp(x);
+  double e = fma(-x, y, 1.0);
+  y = fma(y, e, y);
+  e = fma(-x, y, 1.0);
+  return fma(y, e, y);
+}
+__device__ __forceinline__ double rsq(double x) {
+  double y = __builtin_amdgcn_rsq(x);
+  const double h = 0.5 * x;
+  double r = fma(-h * y, y, 0.5);
+  y = fma(y, r, y);
+  r = fma(-h * y, y, 0.5);
+  return fma(y, r, y);
+}
 __device__ __forceinline__ void sync() { __syncthreads(); }
 
 // packed index of the symmetric 6x6 local (x,y,z,x5,x6,x7) Hessian, a <= b
@@ -106,7 +126,8 @@ enum SumMode { SUM_NEWTON = 0, SUM_LS = 1, SUM_SOC = 2 };
 // phase, accumulated by lane 0 in LDS and written to the two spare rows of the
 // trace buffer.  Never compiled into the product library.
 enum Phase { PH_ROLLOUT, PH_EVAL, PH_DERIVS, PH_ADJ, PH_SUMM, PH_RIC, PH_RESOLVE, PH_FWD, PH_ROWSTEP,
-             PH_BARR, PH_FTB, PH_DFTB, PH_CONV, PH_ACCEPT, PH_INIT, PH_TOTAL, PH_COUNT };
+             PH_BARR, PH_FTB, PH_DFTB, PH_CONV, PH_ACCEPT, PH_INIT, PH_TOTAL,
+             PH_RA, PH_RB, PH_RC, PH_RD, PH_RE, PH_COUNT };
 #ifdef NMPC_STAMPS
 #define STAMP0() const unsigned long long _ts0 = __builtin_amdgcn_s_memtime()
 #define STAMP1(ph) do { const unsigned long long _ts1 = __builtin_amdgcn_s_memtime(); \
@@ -117,25 +138,25 @@ enum Phase { PH_ROLLOUT, PH_EVAL, PH_DERIVS, PH_ADJ, PH_SUMM, PH_RIC, PH_RESOLVE
 #endif
 
 struct Solver {
-  const Params* __restrict__ P;
-  double* sm;
+  const CST Params* __restrict__ P;
+  LDS double* sm;
   int lane, b;
   int N, m, nobs, nw, ng;
   double T;
   // pointers into LDS
-  double *U, *Ut, *dU, *dU2, *zl, *zu, *xl, *xu, *sigx, *ru;
-  double *X, *Xt, *dX, *dX2;
-  double *s, *y, *vl, *vu, *d, *dt, *ds, *ds2, *dc, *dl, *du, *dms;
-  double *gl, *Hl, *trig, *st, *lam;
-  double *K, *kf, *Lc, *Pa, *Pb, *pva, *pvb, *PA, *BtP, *St;
-  double *pp, *obx, *oby, *inc, *filt, *stamps;
+  LDS double* U, *Ut, *dU, *dU2, *zl, *zu, *xl, *xu, *sigx, *ru;
+  LDS double* X, *Xt, *dX, *dX2;
+  LDS double* s, *y, *vl, *vu, *d, *dt, *ds, *ds2, *dc, *dl, *du, *dms;
+  LDS double* gl, *Hl, *trig, *st, *lam;
+  LDS double* K, *kf, *Lc, *Pa, *Pb, *pva, *pvb, *PA, *BtP, *St, *Rt;
+  LDS double* pp, *obx, *oby, *inc, *filt, *stamps;
   // uniform scalars
   double df, mu, tau, delta;
   int nfilt;
   int nzx, nzs;
 
-  __device__ void bind(const Params* prm, double* smem, int lane_, int b_) {
-    P = prm; sm = smem; lane = lane_; b = b_;
+  __device__ __forceinline__ void bind(const Params* prm, double* smem, int lane_, int b_) {
+    P = (const CST Params*)prm; sm = (LDS double*)smem; lane = lane_; b = b_;
     N = prm->N; m = prm->m; nobs = prm->nobs; nw = prm->nw; ng = prm->ng; T = prm->T;
     U = sm + prm->U; Ut = sm + prm->Ut; dU = sm + prm->dU; dU2 = sm + prm->dU2;
     zl = sm + prm->zl; zu = sm + prm->zu; xl = sm + prm->xl; xu = sm + prm->xu;
@@ -148,7 +169,7 @@ struct Solver {
     lam = sm + prm->lam;
     K = sm + prm->K; kf = sm + prm->kf; Lc = sm + prm->Lc;
     Pa = sm + prm->P0; Pb = sm + prm->P1; pva = sm + prm->pv0; pvb = sm + prm->pv1;
-    PA = sm + prm->PA; BtP = sm + prm->BtP; St = sm + prm->St;
+    PA = sm + prm->PA; BtP = sm + prm->BtP; St = sm + prm->St; Rt = sm + prm->Rt;
     pp = sm + prm->p; obx = sm + prm->ob; oby = obx + NMPC_MAX_OBS; inc = sm + prm->inc;
     filt = sm + prm->filt;
     stamps = sm + prm->red;
@@ -161,7 +182,7 @@ struct Solver {
   // X[:,0] = p[0:8]; X[:,k+1] = X[:,k] + T f(X[:,k],U[:,k])   (NMPC_TT.py:160-167)
   // Each lane k sums the increments j<k in order, i.e. bitwise the sequential
   // recursion; the (x,y,z) increments need theta_j, psi_j, so two passes.
-  __device__ void rollout(const double* Us, double* Xd) {
+  __device__ __forceinline__ void rollout(const LDS double* Us, LDS double* Xd) {
     STAMP0();
     const int k = lane;
     if (k < N) {
@@ -193,7 +214,7 @@ struct Solver {
         c1 = c1 + inc[j * 8 + 6];
         c2 = c2 + inc[j * 8 + 7];
       }
-      double* xk = Xd + k * 8;
+      LDS double* xk = Xd + k * 8;
       xk[0] = c0; xk[1] = c1; xk[2] = c2;
 #pragma unroll
       for (int c = 0; c < 5; ++c) xk[3 + c] = a[c];
@@ -205,7 +226,7 @@ struct Solver {
   // ---------------------------------------------------------- stage cost value
   // Literal restatement of NMPC_TT.py:209-220 (same operation order as the
   // oracle's stage_cost).
-  __device__ double stage_cost(const double* x) const {
+  __device__ __forceinline__ double stage_cost(const LDS double* x) const {
     const double hv = P->hv, hh = P->hh;
     const double z = x[2];
     const double a = (z * tan(x[6] + hv) - z * tan(x[6] - hv)) / 2;
@@ -224,7 +245,7 @@ struct Solver {
            P->w2 * ((A * (ex * ex) + Bq * ey * ex + C * (ey * ey)) - 1);
   }
 
-  __device__ __forceinline__ double row_value(const double* x, int i) const {
+  __device__ __forceinline__ double row_value(const LDS double* x, int i) const {
     if (i < 5) return x[boxidx(i)];
     const int o = i - 5;
     const double ddx = x[0] - obx[o], ddy = x[1] - oby[o];
@@ -232,12 +253,12 @@ struct Solver {
   }
 
   // f = sum_k l_k(X) and rows dst[r] = dc[r] * g_r(X) (dc may be null -> unscaled)
-  __device__ double eval_fg(const double* Xs, double* dst, const double* scale) {
+  __device__ __forceinline__ double eval_fg(const LDS double* Xs, LDS double* dst, const LDS double* scale) {
     STAMP0();
     const int k = lane;
     double f = 0.0;
     if (k <= N) {
-      const double* xk = Xs + k * 8;
+      const LDS double* xk = Xs + k * 8;
       if (k < N) f = stage_cost(xk);
       for (int i = 0; i < m; ++i) {
         const int r = k * m + i;
@@ -254,17 +275,17 @@ struct Solver {
   // --------------------------------------------- stage derivatives at X (lane=k)
   // gl[k] = grad l_k (8), Hl[k] = hess l_k packed over (x,y,z,x5,x6,x7), trig[k].
   // Derivation: oracle/nmpc_oracle.py::stage_cost_derivs (Q = (r1/a)^2+(r2/b)^2).
-  __device__ void derivs(const double* Xs, const double* Us) {
+  __device__ __forceinline__ void derivs(const LDS double* Xs, const LDS double* Us) {
     STAMP0();
     const int k = lane;
     if (k <= N) {
-      const double* xk = Xs + k * 8;
+      const LDS double* xk = Xs + k * 8;
       const double th = xk[3], ps = xk[4];
-      double* tg = trig + k * 8;
+      LDS double* tg = trig + k * 8;
       tg[0] = cos(th); tg[1] = sin(th); tg[2] = cos(ps); tg[3] = sin(ps);
       tg[4] = (k < N) ? Us[k * 6] : 0.0;
-      double* g8 = gl + k * 8;
-      double* H = Hl + k * 21;
+      LDS double* g8 = gl + k * 8;
+      LDS double* H = Hl + k * 21;
       if (k == N) {
         for (int i = 0; i < 8; ++i) g8[i] = 0.0;
         for (int i = 0; i < 21; ++i) H[i] = 0.0;
@@ -293,26 +314,28 @@ struct Solver {
         const double r1 = c * ex + sn * ey;
         const double r2 = sn * ex - c * ey;
         double u1[6], u2[6], gr1[6], gr2[6], ge1[6], ge2[6];
-        const double e1 = r1 / a, e2 = r2 / bb;
+        const double ia = 1.0 / a, ib = 1.0 / bb;
+        const double e1 = r1 * ia, e2 = r2 * ib;
 #pragma unroll
         for (int q = 0; q < 6; ++q) {
           u1[q] = -sn * gex[q] + c * gey[q];
           u2[q] = c * gex[q] + sn * gey[q];
           gr1[q] = c * gex[q] + sn * gey[q] - (q == 5 ? r2 : 0.0);
           gr2[q] = sn * gex[q] - c * gey[q] + (q == 5 ? r1 : 0.0);
-          ge1[q] = (gr1[q] - e1 * ga[q]) / a;
-          ge2[q] = (gr2[q] - e2 * gb[q]) / bb;
+          ge1[q] = (gr1[q] - e1 * ga[q]) * ia;
+          ge2[q] = (gr2[q] - e2 * gb[q]) * ib;
         }
         const double ddx = x - xt, ddy = yy - yt;
         const double dd = sqrt(ddx * ddx + ddy * ddy);
-        const double d3 = dd * dd * dd;
+        const double idd = 1.0 / dd;
+        const double id3 = idd * idd * idd;
         const double w1 = P->w1, w2 = P->w2;
         // gradient
         double g6[6];
 #pragma unroll
         for (int q = 0; q < 6; ++q) g6[q] = w2 * (2 * (e1 * ge1[q] + e2 * ge2[q]));
-        g6[0] += w1 * (ddx / dd);
-        g6[1] += w1 * (ddy / dd);
+        g6[0] += w1 * (ddx * idd);
+        g6[1] += w1 * (ddy * idd);
         g8[0] = g6[0]; g8[1] = g6[1]; g8[2] = g6[2]; g8[3] = 0.0; g8[4] = 0.0;
         g8[5] = g6[3]; g8[6] = g6[4]; g8[7] = g6[5];
         // Hessian, 21 packed entries
@@ -329,12 +352,12 @@ struct Solver {
             const double e7a = (qa == 5) ? 1.0 : 0.0, e7b = (qb == 5) ? 1.0 : 0.0;
             const double Hr1 = c * Hex + sn * Hey + e7a * u1[qb] + u1[qa] * e7b - r1 * e7a * e7b;
             const double Hr2 = sn * Hex - c * Hey + e7a * u2[qb] + u2[qa] * e7b - r2 * e7a * e7b;
-            const double He1 = (Hr1 - ge1[qa] * ga[qb] - ga[qa] * ge1[qb] - e1 * Ha) / a;
-            const double He2 = (Hr2 - ge2[qa] * gb[qb] - gb[qa] * ge2[qb] - e2 * Hb) / bb;
+            const double He1 = (Hr1 - ge1[qa] * ga[qb] - ga[qa] * ge1[qb] - e1 * Ha) * ia;
+            const double He2 = (Hr2 - ge2[qa] * gb[qb] - gb[qa] * ge2[qb] - e2 * Hb) * ib;
             double h = w2 * (2 * (ge1[qa] * ge1[qb] + ge2[qa] * ge2[qb] + e1 * He1 + e2 * He2));
-            if (qa == 0 && qb == 0) h += w1 * (ddy * ddy / d3);
-            if (qa == 0 && qb == 1) h += w1 * (-ddx * ddy / d3);
-            if (qa == 1 && qb == 1) h += w1 * (ddx * ddx / d3);
+            if (qa == 0 && qb == 0) h += w1 * (ddy * ddy * id3);
+            if (qa == 0 && qb == 1) h += w1 * (-ddx * ddy * id3);
+            if (qa == 1 && qb == 1) h += w1 * (ddx * ddx * id3);
             H[hp(qa, qb)] = h;
           }
         }
@@ -348,7 +371,7 @@ struct Solver {
   __device__ __forceinline__ void stage_AB(int k, double& E03, double& E04, double& E13,
                                            double& E14, double& E23, double& b00, double& b10,
                                            double& b20) const {
-    const double* tg = trig + k * 8;
+    const LDS double* tg = trig + k * 8;
     const double ct = tg[0], stt = tg[1], cp = tg[2], sp = tg[3], v = tg[4];
     E03 = -T * v * cp * stt; E04 = -T * v * sp * ct;
     E13 = -T * v * sp * stt; E14 = T * v * cp * ct;
@@ -359,13 +382,13 @@ struct Solver {
   // --------------------------------------------- adjoint lam_k (lane = k)
   // lam_N = G_N^T y_N; lam_k = ofac*gl_k + G_k^T y_k + A_k^T lam_{k+1}
   // (oracle SSEval.hessian).  yy may be null (objective only).
-  __device__ void adjoint(double ofac, const double* yy) {
+  __device__ __forceinline__ void adjoint(double ofac, const LDS double* yy) {
     STAMP0();
     const int k = lane;
-    double* wv = inc;  // scratch 8*(N+1)
+    LDS double* wv = inc;  // scratch 8*(N+1)
     if (k <= N) {
       double w[8];
-      const double* xk = X + k * 8;
+      const LDS double* xk = X + k * 8;
 #pragma unroll
       for (int i = 0; i < 8; ++i) w[i] = ofac * gl[k * 8 + i];
       if (yy) {
@@ -376,10 +399,10 @@ struct Solver {
         for (int o = 0; o < nobs; ++o) {
           const int r = k * m + 5 + o;
           const double ddx = xk[0] - obx[o], ddy = xk[1] - oby[o];
-          const double dd = sqrt(ddx * ddx + ddy * ddy);
+          const double idd = rsq(ddx * ddx + ddy * ddy);
           const double cy = dc[r] * yy[r];
-          w[0] += cy * (-(ddx / dd));
-          w[1] += cy * (-(ddy / dd));
+          w[0] += cy * (-(ddx * idd));
+          w[1] += cy * (-(ddy * idd));
         }
       }
 #pragma unroll
@@ -402,7 +425,7 @@ struct Solver {
       for (int j = N - 1; j >= k; --j) {
         double E03, E04, E13, E14, E23, b00, b10, b20;
         stage_AB(j, E03, E04, E13, E14, E23, b00, b10, b20);
-        const double* ln = lam + (j + 1) * 8;
+        const LDS double* ln = lam + (j + 1) * 8;
         a3 = wv[j * 8 + 3] + (((E03 * ln[0] + E13 * ln[1]) + E23 * ln[2]) + a3);
         a4 = wv[j * 8 + 4] + ((E04 * ln[0] + E14 * ln[1]) + a4);
       }
@@ -416,9 +439,9 @@ struct Solver {
   // dL/du_k[c] = (B_k^T lam_{k+1})[c]
   __device__ __forceinline__ double grad_u(int i) const {
     const int k = i / 6, c = i - 6 * (i / 6);
-    const double* ln = lam + (k + 1) * 8;
+    const LDS double* ln = lam + (k + 1) * 8;
     if (c == 0) {
-      const double* tg = trig + k * 8;
+      const LDS double* tg = trig + k * 8;
       const double ct = tg[0], stt = tg[1], cp = tg[2], sp = tg[3];
       return (T * cp * ct) * ln[0] + (T * sp * ct) * ln[1] + (T * stt) * ln[2];
     }
@@ -426,11 +449,11 @@ struct Solver {
   }
 
   // ------------------------------------------------ slacks / barrier helpers
-  __device__ __forceinline__ double sl_x(int i, const double* u) const { return u[i] - xl[i]; }
-  __device__ __forceinline__ double su_x(int i, const double* u) const { return xu[i] - u[i]; }
+  __device__ __forceinline__ double sl_x(int i, const LDS double* u) const { return u[i] - xl[i]; }
+  __device__ __forceinline__ double su_x(int i, const LDS double* u) const { return xu[i] - u[i]; }
 
   // barrier objective phi (oracle barrier_obj) at (u, s + a*ds) [sv == null -> s]
-  __device__ double barrier_obj(double f, const double* u, const double* sb, const double* dsv,
+  __device__ __forceinline__ double barrier_obj(double f, const LDS double* u, const LDS double* sb, const LDS double* dsv,
                                 double a) const {
     STAMP0();
     double logs = 0.0, damp = 0.0;
@@ -462,11 +485,11 @@ struct Solver {
   //  NEWTON: Q += Gt^T D Gt + sum_obs y dc Hg ; q += Gt^T (y + D rd + rs)
   //  SOC:    q only, with rd := dms
   //  LS:     Q += Gt^T Gt ; q += -Gt^T (vu - vl)           (least-squares y init)
-  __device__ void summaries(int mode) {
+  __device__ __forceinline__ void summaries(int mode) {
     STAMP0();
     const int k = lane;
     if (k <= N) {
-      const double* xk = X + k * 8;
+      const LDS double* xk = X + k * 8;
       double Qxy0 = 0, Qxy1 = 0, Qxy2 = 0, qx = 0, qy = 0;
       double Qb[5], qb[5];
       const double kd = P->o.kappa_d;
@@ -478,10 +501,10 @@ struct Solver {
           Bw = -(vu[r] - vl[r]);
         } else {
           const bool lo = hasl(dl[r]), hi = hasu(du[r]);
-          const double Sl = lo ? s[r] - dl[r] : 1.0, Su = hi ? du[r] - s[r] : 1.0;
-          const double sig = (lo ? vl[r] / Sl : 0.0) + (hi ? vu[r] / Su : 0.0);
+          const double iSl = lo ? rcp(s[r] - dl[r]) : 0.0, iSu = hi ? rcp(du[r] - s[r]) : 0.0;
+          const double sig = vl[r] * iSl + vu[r] * iSu;
           const double D = sig + delta;
-          const double rs = -y[r] - (lo ? mu / Sl : 0.0) + (hi ? mu / Su : 0.0) +
+          const double rs = -y[r] - mu * iSl + mu * iSu +
                             kd * mu * ((lo && !hi ? 1.0 : 0.0) - (hi && !lo ? 1.0 : 0.0));
           const double rd = (mode == SUM_SOC) ? dms[r] : d[r] - s[r];
           A = D;
@@ -494,18 +517,18 @@ struct Solver {
         } else {
           const int o = i - 5;
           const double ddx = xk[0] - obx[o], ddy = xk[1] - oby[o];
-          const double dd = sqrt(ddx * ddx + ddy * ddy);
-          const double gx = -(ddx / dd), gy = -(ddy / dd);
-          const double d3 = dd * dd * dd;
+          const double idd = rsq(ddx * ddx + ddy * ddy);
+          const double gx = -(ddx * idd), gy = -(ddy * idd);
+          const double id3 = idd * idd * idd;
           const double w = dc[r] * dc[r] * A;
-          Qxy0 += w * gx * gx + C * (-ddy * ddy / d3);
-          Qxy1 += w * gx * gy + C * (ddx * ddy / d3);
-          Qxy2 += w * gy * gy + C * (-ddx * ddx / d3);
+          Qxy0 += w * gx * gx + C * (-ddy * ddy * id3);
+          Qxy1 += w * gx * gy + C * (ddx * ddy * id3);
+          Qxy2 += w * gy * gy + C * (-ddx * ddx * id3);
           qx += dc[r] * Bw * gx;
           qy += dc[r] * Bw * gy;
         }
       }
-      double* o16 = st + k * 16;
+      LDS double* o16 = st + k * 16;
       o16[0] = Qxy0; o16[1] = Qxy1; o16[2] = Qxy2;
 #pragma unroll
       for (int i = 0; i < 5; ++i) { o16[3 + i] = Qb[i]; o16[10 + i] = qb[i]; }
@@ -520,7 +543,7 @@ struct Solver {
     double q = 0.0;
     const int vi = vloc(i), vj = vloc(j);
     if (vi >= 0 && vj >= 0) q += hfac * Hl[k * 21 + hp(vi, vj)];
-    const double* o16 = st + k * 16;
+    const LDS double* o16 = st + k * 16;
     if (i < 2 && j < 2) q += o16[i + j];  // Qxy0 (0,0), Qxy1 (0,1)/(1,0), Qxy2 (1,1)
     if (i == j) {
       if (i == 2) q += o16[3];
@@ -528,9 +551,9 @@ struct Solver {
       else if (i >= 5) q += o16[i + 0];  // 5->o16[5], 6->o16[6], 7->o16[7]
     }
     if (dyn && k < N && (i == 3 || i == 4) && (j == 3 || j == 4)) {
-      const double* tg = trig + k * 8;
+      const LDS double* tg = trig + k * 8;
       const double ct = tg[0], stt = tg[1], cp = tg[2], sp = tg[3], v = tg[4];
-      const double* ln = lam + (k + 1) * 8;
+      const LDS double* ln = lam + (k + 1) * 8;
       const double l0 = ln[0], l1 = ln[1], l2 = ln[2];
       if (i == 3 && j == 3) q += T * (-l0 * v * cp * ct - l1 * v * sp * ct - l2 * v * stt);
       else if (i == 4 && j == 4) q += T * (-l0 * v * cp * ct - l1 * v * sp * ct);
@@ -540,7 +563,7 @@ struct Solver {
   }
   __device__ __forceinline__ double qentry(int k, int i, double gfac) const {
     double q = gfac * gl[k * 8 + i];
-    const double* o16 = st + k * 16;
+    const LDS double* o16 = st + k * 16;
     if (i == 0) q += o16[8];
     else if (i == 1) q += o16[9];
     else if (i == 2) q += o16[10];
@@ -550,9 +573,9 @@ struct Solver {
   }
   // S_k[0][3], S_k[0][4] (dynamics cross terms, oracle dyn_hess Hxu)
   __device__ __forceinline__ void Sdyn(int k, double& s03, double& s04) const {
-    const double* tg = trig + k * 8;
+    const LDS double* tg = trig + k * 8;
     const double ct = tg[0], stt = tg[1], cp = tg[2], sp = tg[3];
-    const double* ln = lam + (k + 1) * 8;
+    const LDS double* ln = lam + (k + 1) * 8;
     const double l0 = ln[0], l1 = ln[1], l2 = ln[2];
     s03 = T * (-l0 * cp * stt - l1 * sp * stt + l2 * ct);
     s04 = T * (-l0 * sp * ct + l1 * cp * ct);
@@ -564,18 +587,18 @@ struct Solver {
   // (wrong inertia).  Stores K_k, k_k, chol(R~_k) for the forward sweep / SOC.
   //   hfac, gfac: factors on the stage cost Hessian / gradient; dyn: add the
   //   dynamics second derivatives; Rd: diag of R (null -> 1).
-  __device__ bool riccati(double hfac, double gfac, bool dyn, const double* Rd, const double* rv) {
+  __device__ __forceinline__ bool riccati(double hfac, double gfac, bool dyn, const LDS double* Rd, const LDS double* rv) {
     STAMP0();
     const bool r = riccati_(hfac, gfac, dyn, Rd, rv);
     STAMP1(PH_RIC);
     return r;
   }
-  __device__ bool riccati_(double hfac, double gfac, bool dyn, const double* Rd, const double* rv) {
+  __device__ __forceinline__ bool riccati_(double hfac, double gfac, bool dyn, const LDS double* Rd, const LDS double* rv) {
     const int i = lane >> 3, j = lane & 7;
-    double* Pc = Pa;
-    double* Pn = Pb;
-    double* pc = pva;
-    double* pn = pvb;
+    LDS double* Pc = Pa;
+    LDS double* Pn = Pb;
+    LDS double* pc = pva;
+    LDS double* pn = pvb;
     Pc[lane] = Qentry(N, i, j, hfac, dyn);
     if (lane < 8) pc[lane] = qentry(N, lane, gfac);
     sync();
@@ -584,8 +607,9 @@ struct Solver {
       double E03, E04, E13, E14, E23, b00, b10, b20;
       stage_AB(k, E03, E04, E13, E14, E23, b00, b10, b20);
       // (A) PA = P A ; BtP = B^T P
+      { STAMP0();
       {
-        const double* Pi = Pc + i * 8;
+        const LDS double* Pi = Pc + i * 8;
         double v = Pi[j];
         if (j == 3) v = v + ((Pi[0] * E03 + Pi[1] * E13) + Pi[2] * E23);
         else if (j == 4) v = v + (Pi[0] * E04 + Pi[1] * E14);
@@ -597,8 +621,10 @@ struct Solver {
         }
       }
       sync();
+      STAMP1(PH_RA); }
       // (B) APA = A^T P A (register) ; St = S + B^T P A
       double APA;
+      { STAMP0();
       {
         double v = PA[lane];
         if (i == 3) v = v + ((E03 * PA[j] + E13 * PA[8 + j]) + E23 * PA[16 + j]);
@@ -615,37 +641,40 @@ struct Solver {
           }
           St[lane] = sv;
         }
+        if (lane >= 48 || lane < 5) {  // 21 lanes build R~ = R + B^T P B (packed lower)
+          const int t = lane >= 48 ? lane - 48 : 16 + lane;
+          int r = 0;
+          while ((r + 1) * (r + 2) / 2 <= t) ++r;
+          const int c = t - r * (r + 1) / 2;
+          double v = (c == 0) ? ((BtP[r * 8 + 0] * b00 + BtP[r * 8 + 1] * b10) + BtP[r * 8 + 2] * b20)
+                              : T * BtP[r * 8 + 2 + c];
+          if (r == c) v += (Rd ? Rd[k * 6 + r] : 1.0) + delta;
+          Rt[t] = v;
+        }
       }
       sync();
-      // (C) every lane: R~ = R + B^T P B, Cholesky, r~ = r + B^T p
+      STAMP1(PH_RB); }
+      // (C) every lane: Cholesky of R~ (pivots by rsqrt), r~ = r + B^T p
+      STAMP0();
       double Lm[21], idg[6], rt[6];
       {
-        double R[21];
 #pragma unroll
-        for (int r = 0; r < 6; ++r) {
-#pragma unroll
-          for (int c = 0; c <= r; ++c) {
-            double v = (c == 0) ? ((BtP[r * 8 + 0] * b00 + BtP[r * 8 + 1] * b10) + BtP[r * 8 + 2] * b20)
-                                : T * BtP[r * 8 + 2 + c];
-            if (r == c) v += (Rd ? Rd[k * 6 + r] : 1.0) + delta;
-            R[r * (r + 1) / 2 + c] = v;
-          }
-        }
+        for (int t = 0; t < 21; ++t) Lm[t] = Rt[t];
 #pragma unroll
         for (int c = 0; c < 6; ++c) {
-          double dg = R[c * (c + 1) / 2 + c];
+          double dg = Lm[c * (c + 1) / 2 + c];
 #pragma unroll
           for (int t = 0; t < c; ++t) dg -= Lm[c * (c + 1) / 2 + t] * Lm[c * (c + 1) / 2 + t];
           if (!(dg > 0.0)) ok = false;
-          const double l = sqrt(dg);
-          Lm[c * (c + 1) / 2 + c] = l;
-          idg[c] = 1.0 / l;
+          const double ig = rsq(dg);
+          Lm[c * (c + 1) / 2 + c] = dg * ig;
+          idg[c] = ig;
 #pragma unroll
           for (int r = c + 1; r < 6; ++r) {
-            double v = R[r * (r + 1) / 2 + c];
+            double v = Lm[r * (r + 1) / 2 + c];
 #pragma unroll
             for (int t = 0; t < c; ++t) v -= Lm[r * (r + 1) / 2 + t] * Lm[c * (c + 1) / 2 + t];
-            Lm[r * (r + 1) / 2 + c] = v * idg[c];
+            Lm[r * (r + 1) / 2 + c] = v * ig;
           }
         }
         // r~ = r_k + B^T p_{k+1}
@@ -653,9 +682,11 @@ struct Solver {
 #pragma unroll
         for (int r = 1; r < 6; ++r) rt[r] = rv[k * 6 + r] + T * pc[2 + r];
       }
+      STAMP1(PH_RC);
       ok = !wany(!ok);  // every lane computed the same pivots; make it explicit
       if (!ok) break;
       // (D) K = -R~^{-1} St (lanes 0..7 one column each), kf = -R~^{-1} r~
+      { STAMP0();
       {
         if (lane < 9) {
           double v[6];
@@ -686,7 +717,7 @@ struct Solver {
           }
         }
         if (lane == 9) {
-          double* lc = Lc + k * 28;
+          LDS double* lc = Lc + k * 28;
 #pragma unroll
           for (int t = 0; t < 21; ++t) lc[t] = Lm[t];
 #pragma unroll
@@ -694,7 +725,9 @@ struct Solver {
         }
       }
       sync();
+      STAMP1(PH_RD); }
       // (E) P_k = Q_k + A^T P A + St^T K ; p_k = q_k + A^T p + K^T r~
+      { STAMP0();
       {
         double sk = 0.0;
 #pragma unroll
@@ -711,14 +744,15 @@ struct Solver {
         }
       }
       sync();
-      double* t1 = Pc; Pc = Pn; Pn = t1;
-      double* t2 = pc; pc = pn; pn = t2;
+      STAMP1(PH_RE); }
+      LDS double* t1 = Pc; Pc = Pn; Pn = t1;
+      LDS double* t2 = pc; pc = pn; pn = t2;
     }
     return ok;
   }
 
   // gradient-only re-solve with the stored factors (second-order correction)
-  __device__ void resolve(double gfac, const double* rv) {
+  __device__ __forceinline__ void resolve(double gfac, const LDS double* rv) {
     STAMP0();
     // every lane runs the vector recursion redundantly (no LDS exchange)
     double p8[8];
@@ -727,7 +761,7 @@ struct Solver {
     for (int k = N - 1; k >= 0; --k) {
       double E03, E04, E13, E14, E23, b00, b10, b20;
       stage_AB(k, E03, E04, E13, E14, E23, b00, b10, b20);
-      const double* lc = Lc + k * 28;
+      const LDS double* lc = Lc + k * 28;
       double rt[6], v[6];
       rt[0] = rv[k * 6 + 0] + ((b00 * p8[0] + b10 * p8[1]) + b20 * p8[2]);
 #pragma unroll
@@ -770,7 +804,7 @@ struct Solver {
 
   // forward sweep: du_k = K_k dx_k + k_k ; dx_{k+1} = A_k dx_k + B_k du_k
   // (redundant in every lane, broadcast LDS reads; lane 0 stores)
-  __device__ void forward(double* dUo, double* dXo) {
+  __device__ __forceinline__ void forward(LDS double* dUo, LDS double* dXo) {
     STAMP0();
     double dx[8];
 #pragma unroll
@@ -807,20 +841,20 @@ struct Solver {
   }
 
   // ds_r = Gt_r dX_k + rd_r (J dU = G Z dU = G dX)
-  __device__ void row_step(const double* dXs, const double* rdsrc, bool rd_is_dms, double* dso) {
+  __device__ __forceinline__ void row_step(const LDS double* dXs, const LDS double* rdsrc, bool rd_is_dms, LDS double* dso) {
     STAMP0();
     for (int r = lane; r < ng; r += WAVE) {
       const int k = r / m, i = r - k * m;
-      const double* xk = X + k * 8;
-      const double* dxk = dXs + k * 8;
+      const LDS double* xk = X + k * 8;
+      const LDS double* dxk = dXs + k * 8;
       double jd;
       if (i < 5) {
         jd = dc[r] * dxk[boxidx(i)];
       } else {
         const int o = i - 5;
         const double ddx = xk[0] - obx[o], ddy = xk[1] - oby[o];
-        const double dd = sqrt(ddx * ddx + ddy * ddy);
-        jd = dc[r] * ((-(ddx / dd)) * dxk[0] + (-(ddy / dd)) * dxk[1]);
+        const double idd = rsq(ddx * ddx + ddy * ddy);
+        jd = dc[r] * ((-(ddx * idd)) * dxk[0] + (-(ddy * idd)) * dxk[1]);
       }
       const double rd = rd_is_dms ? rdsrc[r] : d[r] - s[r];
       dso[r] = jd + rd;
@@ -830,7 +864,7 @@ struct Solver {
   }
 
   // primal fraction to the boundary (oracle frac_to_bound)
-  __device__ double frac_to_bound(double tau_, const double* dUs, const double* dss) const {
+  __device__ __forceinline__ double frac_to_bound(double tau_, const LDS double* dUs, const LDS double* dss) const {
     STAMP0();
     double a = 1.0;
     for (int i = lane; i < nw; i += WAVE) {
@@ -851,15 +885,15 @@ struct Solver {
   // dual step components (oracle solve_dir) -- current slacks
   __device__ __forceinline__ void dz_x(int i, double dx, double& dzl, double& dzu) const {
     dzl = 0.0; dzu = 0.0;
-    if (hasl(xl[i])) { const double S = U[i] - xl[i]; dzl = mu / S - zl[i] - zl[i] / S * dx; }
-    if (hasu(xu[i])) { const double S = xu[i] - U[i]; dzu = mu / S - zu[i] + zu[i] / S * dx; }
+    if (hasl(xl[i])) { const double iS = rcp(U[i] - xl[i]); dzl = mu * iS - zl[i] - zl[i] * iS * dx; }
+    if (hasu(xu[i])) { const double iS = rcp(xu[i] - U[i]); dzu = mu * iS - zu[i] + zu[i] * iS * dx; }
   }
   __device__ __forceinline__ void dv_s(int r, double dsv, double& dvl, double& dvu) const {
     dvl = 0.0; dvu = 0.0;
-    if (hasl(dl[r])) { const double S = s[r] - dl[r]; dvl = mu / S - vl[r] - vl[r] / S * dsv; }
-    if (hasu(du[r])) { const double S = du[r] - s[r]; dvu = mu / S - vu[r] + vu[r] / S * dsv; }
+    if (hasl(dl[r])) { const double iS = rcp(s[r] - dl[r]); dvl = mu * iS - vl[r] - vl[r] * iS * dsv; }
+    if (hasu(du[r])) { const double iS = rcp(du[r] - s[r]); dvu = mu * iS - vu[r] + vu[r] * iS * dsv; }
   }
-  __device__ double dual_frac_to_bound(double tau_, const double* dUs, const double* dss) const {
+  __device__ __forceinline__ double dual_frac_to_bound(double tau_, const LDS double* dUs, const LDS double* dss) const {
     STAMP0();
     double a = 1.0;
     for (int i = lane; i < nw; i += WAVE) {
@@ -882,14 +916,14 @@ struct Solver {
   // rs_r (oracle rs) and D_r
   __device__ __forceinline__ void row_rs(int r, double& D, double& rs) const {
     const bool lo = hasl(dl[r]), hi = hasu(du[r]);
-    const double Sl = lo ? s[r] - dl[r] : 1.0, Su = hi ? du[r] - s[r] : 1.0;
-    D = (lo ? vl[r] / Sl : 0.0) + (hi ? vu[r] / Su : 0.0) + delta;
-    rs = -y[r] - (lo ? mu / Sl : 0.0) + (hi ? mu / Su : 0.0) +
+    const double iSl = lo ? rcp(s[r] - dl[r]) : 0.0, iSu = hi ? rcp(du[r] - s[r]) : 0.0;
+    D = vl[r] * iSl + vu[r] * iSu + delta;
+    rs = -y[r] - mu * iSl + mu * iSu +
          P->o.kappa_d * mu * ((lo && !hi ? 1.0 : 0.0) - (hi && !lo ? 1.0 : 0.0));
   }
 
   // complementarity max |S z - mu_| over all bounds
-  __device__ double compl_max(double mu_) const {
+  __device__ __forceinline__ double compl_max(double mu_) const {
     double c = 0.0;
     for (int i = lane; i < nw; i += WAVE) {
       if (hasl(xl[i])) c = fmax(c, fabs((U[i] - xl[i]) * zl[i] - mu_));
@@ -903,14 +937,14 @@ struct Solver {
   }
 
   // filter
-  __device__ bool filter_ok(double phi, double th) const {
+  __device__ __forceinline__ bool filter_ok(double phi, double th) const {
     bool ok = true;
     for (int e = lane; e < nfilt; e += WAVE) {
       if (!(phi <= filt[2 * e] || th <= filt[2 * e + 1])) ok = false;
     }
     return !wany(!ok);
   }
-  __device__ void filter_add(double phi, double th) {
+  __device__ __forceinline__ void filter_add(double phi, double th) {
     // drop entries dominated by the new one, then append (IpFilter::AddEntry)
     sync();
     if (lane == 0) {
@@ -934,7 +968,7 @@ struct Solver {
 
   // trial point u = U + a dUs, s = s + a dss: rollout into Xt, rows into dt.
   // returns false on an evaluation error (NaN/Inf)
-  __device__ bool trial(double a, const double* dUs, const double* dss, double& ft, double& phit,
+  __device__ __forceinline__ bool trial(double a, const LDS double* dUs, const LDS double* dss, double& ft, double& phit,
                         double& tht) {
     for (int i = lane; i < nw; i += WAVE) Ut[i] = U[i] + a * dUs[i];
     sync();
@@ -963,14 +997,14 @@ __global__ __launch_bounds__(WAVE) void nmpc_solve_kernel(const Params* __restri
   const int lane = threadIdx.x;
   Solver S;
   S.bind(prm, smem, lane, b);
-  double* stamps = S.stamps;
+  LDS double* stamps = S.stamps;
   if (lane < PH_COUNT) stamps[lane] = 0.0;
   const unsigned long long _tk0 = __builtin_amdgcn_s_memtime();
   (void)_tk0;
   const nmpc_options& o = prm->o;
   const int N = S.N, nw = S.nw, ng = S.ng, m = S.m;
   const int max_iter = o.max_iter;
-  double* trace = io.trace ? io.trace + (long long)b * (max_iter + 2) * TRACE_F : nullptr;
+  double* trace = io.trace ? io.trace + (long long)b * (max_iter + 3) * TRACE_F : nullptr;
 
   // ---------------- load scenario data
   for (int i = lane; i < prm->np; i += WAVE) S.pp[i] = io.p[(long long)b * io.ld_p + i];
@@ -1032,7 +1066,7 @@ __global__ __launch_bounds__(WAVE) void nmpc_solve_kernel(const Params* __restri
       double rmax[5 + NMPC_MAX_OBS];
       for (int i = 0; i < m; ++i) rmax[i] = 0.0;
       if (k <= N && k >= 1) {
-        const double* xk = S.X + k * 8;
+        const LDS double* xk = S.X + k * 8;
         double gxo[NMPC_MAX_OBS], gyo[NMPC_MAX_OBS];
         for (int q = 0; q < S.nobs; ++q) {
           const double ddx = xk[0] - S.obx[q], ddy = xk[1] - S.oby[q];
@@ -1124,8 +1158,8 @@ __global__ __launch_bounds__(WAVE) void nmpc_solve_kernel(const Params* __restri
       for (int r = lane; r < ng; r += WAVE) {
         // y = bs - J wx with J wx = Gt dX
         const int k = r / m, i = r - k * m;
-        const double* xk = S.X + k * 8;
-        const double* dxk = S.dX + k * 8;
+        const LDS double* xk = S.X + k * 8;
+        const LDS double* dxk = S.dX + k * 8;
         double jd;
         if (i < 5) jd = S.dc[r] * dxk[boxidx(i)];
         else {
@@ -1374,7 +1408,7 @@ __global__ __launch_bounds__(WAVE) void nmpc_solve_kernel(const Params* __restri
       sync();
       S.derivs(S.Xt, S.Ut);
       // adjoint at the trial point: swap X temporarily
-      double* Xs = S.X; S.X = S.Xt;
+      LDS double* Xs = S.X; S.X = S.Xt;
       S.adjoint(S.df, S.dms);
       S.X = Xs;
       double dual2 = 0, prim2 = 0, cm2 = 0;
@@ -1453,7 +1487,7 @@ __global__ __launch_bounds__(WAVE) void nmpc_solve_kernel(const Params* __restri
             for (int r = lane; r < ng; r += WAVE) S.dms[r] = S.d[r] - S.s[r];
             int cnt = 0;
             bool soc_acc = false;
-            const double* dsp = S.ds;  // step whose trial is in Ut/dt
+            const LDS double* dsp = S.ds;  // step whose trial is in Ut/dt
             while (cnt < o.max_soc && (cnt == 0 || th_tr <= o.kappa_soc * th_old)) {
               th_old = th_tr;
               for (int r = lane; r < ng; r += WAVE) {
@@ -1498,8 +1532,8 @@ __global__ __launch_bounds__(WAVE) void nmpc_solve_kernel(const Params* __restri
     // ===== accept the trial point (IpoptAlgorithm::AcceptTrialPoint)
     {
       STAMP0();
-      const double* dUa = (acc_kind == 2) ? S.dU2 : S.dU;
-      const double* dsa = (acc_kind == 2) ? S.ds2 : S.ds;
+      const LDS double* dUa = (acc_kind == 2) ? S.dU2 : S.dU;
+      const LDS double* dsa = (acc_kind == 2) ? S.ds2 : S.ds;
       if (acc_kind != 3) alpha_d = S.dual_frac_to_bound(tau, dUa, dsa);
       const double ap = alpha_p, ad = alpha_d;
       const double ks = o.kappa_sigma;
@@ -1652,7 +1686,7 @@ static int layout(Params& P) {
   P.ds = al(ng); P.ds2 = al(ng); P.dc = al(ng); P.dl = al(ng); P.du = al(ng); P.dms = al(ng);
   P.gl = al(8 * NS); P.Hl = al(21 * NS); P.trig = al(8 * NS); P.st = al(16 * NS); P.lam = al(8 * NS);
   P.K = al(48 * P.N); P.kf = al(6 * P.N); P.Lc = al(28 * P.N);
-  P.P0 = al(64); P.P1 = al(64); P.pv0 = al(8); P.pv1 = al(8); P.PA = al(64); P.BtP = al(48); P.St = al(48);
+  P.P0 = al(64); P.P1 = al(64); P.pv0 = al(8); P.pv1 = al(8); P.PA = al(64); P.BtP = al(48); P.St = al(48); P.Rt = al(22);
   P.p = al(64); P.ob = al(2 * NMPC_MAX_OBS); P.inc = al(8 * 64); P.filt = al(2 * FCAP + 2); P.red = al(64);
   P.total = off;
   return off * 8;
@@ -1761,7 +1795,7 @@ int nmpc_set_trace(nmpc_handle* h, int32_t enable) {
 int nmpc_read_trace(nmpc_handle* h, int32_t B, double* host_out) {
   if (!h || !host_out) return fail(NMPC_E_INVALID, "null argument");
   if (!h->dtrace || B > h->last_B) return fail(NMPC_E_INVALID, "no trace recorded for that batch");
-  const size_t n = (size_t)B * (h->hp.o.max_iter + 2) * TRACE_F;
+  const size_t n = (size_t)B * (h->hp.o.max_iter + 3) * TRACE_F;
   if (hipMemcpy(host_out, h->dtrace, n * sizeof(double), hipMemcpyDeviceToHost) != hipSuccess)
     return fail(NMPC_E_HIP, "hipMemcpy trace");
   return NMPC_OK;
@@ -1787,7 +1821,7 @@ int nmpc_solve_batch_dev(nmpc_handle* h, int32_t B, const double* x0, int64_t ld
   io.x_out = x_out; io.f_out = f_out; io.g_out = g_out; io.lam_x = lam_x_out; io.lam_g = lam_g_out;
   io.X_out = X_out; io.status = status; io.iters = iters; io.trace = nullptr;
   if (h->trace) {
-    const size_t need = (size_t)B * (P.o.max_iter + 2) * TRACE_F * sizeof(double);
+    const size_t need = (size_t)B * (P.o.max_iter + 3) * TRACE_F * sizeof(double);
     if (need > h->trace_bytes) {
       if (h->dtrace) hipFree(h->dtrace);
       h->dtrace = nullptr; h->trace_bytes = 0;

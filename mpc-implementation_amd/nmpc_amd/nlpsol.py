@@ -226,7 +226,7 @@ class Solver:
         _lib.check(_lib.lib().nmpc_set_trace(self._h, int(enable)))
 
     def read_trace(self, B: int) -> np.ndarray:
-        buf = np.zeros((B, self.max_iter + 2, _lib.TRACE_FIELDS))
+        buf = np.zeros((B, self.max_iter + 3, _lib.TRACE_FIELDS))
         _lib.check(_lib.lib().nmpc_read_trace(self._h, B, _dptr(buf)))
         return buf
 
