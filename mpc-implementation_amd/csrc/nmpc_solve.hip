@@ -38,6 +38,7 @@ namespace {
 constexpr int WAVE = 64;
 #define LDS __attribute__((address_space(3)))
 #define CST __attribute__((address_space(4)))
+#define GLB __attribute__((address_space(1)))
 constexpr double BIGB = 1e19;  // IPOPT nlp_{lower,upper}_bound_inf
 constexpr int FCAP = 128;      // filter capacity (>= max_iter of the reference opts)
 constexpr int TRACE_F = NMPC_TRACE_FIELDS;
@@ -53,14 +54,52 @@ struct Params {
   double ox[NMPC_MAX_OBS], oy[NMPC_MAX_OBS], orr[NMPC_MAX_OBS];
   int oxp[NMPC_MAX_OBS], oyp[NMPC_MAX_OBS];
   nmpc_options o;
-  // LDS layout, offsets in doubles
+};
+
+// Per-scenario memory layout (offsets in doubles).  Computed at compile time
+// for a capacity class (NMAX, MMAX) so every array address folds into a base
+// register plus an immediate: no pointer registers in the kernel.
+struct Lay {
+  // global workspace (64 B aligned slices)
   int U, Ut, dU, dU2, zl, zu, xl, xu, sigx, ru;
-  int X, Xt, dX, dX2;
-  int s, y, vl, vu, d, dt, ds, ds2, dc, dl, du, dms;
-  int gl, Hl, trig, st, lam;
-  int K, kf, Lc, P0, P1, pv0, pv1, PA, BtP, St, Rt;
-  int p, ob, inc, filt, red;
-  int total;
+  int s, y, vl, vu, d, dt, ds, ds2, dc, dl, du, dms, filt;
+  int gl, Hl, Qs, K, Rk;        // stage data / Riccati factors (global copies)
+  // LDS
+  int X, Xt, dX;
+  int trig, qs, lam;
+  int Kc, kf, Rc, P0, P1, pv0, pv1, St;
+  int p, ob, inc, red;
+  int total;    // LDS doubles per scenario
+  int wstotal;  // global-workspace doubles per scenario
+};
+constexpr int al2(int n) { return (n + 1) & ~1; }
+constexpr int al8(int n) { return (n + 7) & ~7; }
+constexpr Lay make_layout(int N, int m) {
+  Lay L{};
+  const int nw = 6 * N, ng = m * (N + 1), nX = 8 * (N + 1), NS = N + 1;
+  int g = 0, o = 0;
+  L.U = g; g += al8(nw); L.Ut = g; g += al8(nw); L.dU = g; g += al8(nw); L.dU2 = g; g += al8(nw);
+  L.zl = g; g += al8(nw); L.zu = g; g += al8(nw); L.xl = g; g += al8(nw); L.xu = g; g += al8(nw);
+  L.sigx = g; g += al8(nw); L.ru = g; g += al8(nw);
+  L.s = g; g += al8(ng); L.y = g; g += al8(ng); L.vl = g; g += al8(ng); L.vu = g; g += al8(ng);
+  L.d = g; g += al8(ng); L.dt = g; g += al8(ng); L.ds = g; g += al8(ng); L.ds2 = g; g += al8(ng);
+  L.dc = g; g += al8(ng); L.dl = g; g += al8(ng); L.du = g; g += al8(ng); L.dms = g; g += al8(ng);
+  L.filt = g; g += al8(2 * FCAP + 2);
+  L.gl = g; g += al8(8 * NS); L.Hl = g; g += al8(21 * NS); L.Qs = g; g += al8(36 * NS);
+  L.K = g; g += al8(48 * N); L.Rk = g; g += al8(21 * N);
+  L.wstotal = g;
+  L.X = o; o += al2(nX); L.Xt = o; o += al2(nX); L.dX = o; o += al2(nX);
+  L.trig = o; o += al2(8 * NS); L.qs = o; o += al2(10 * NS); L.lam = o; o += al2(8 * NS);
+  L.Kc = o; o += 48; L.kf = o; o += al2(6 * N); L.Rc = o; o += 22;
+  L.P0 = o; o += 64; L.P1 = o; o += 64; L.pv0 = o; o += 8; L.pv1 = o; o += 8; L.St = o; o += 48;
+  L.p = o; o += 64; L.ob = o; o += al2(2 * NMPC_MAX_OBS); L.inc = o; o += al2(8 * NS); L.red = o; o += 24;
+  L.total = o;
+  return L;
+}
+template <int NMAX, int MMAX>
+struct Cap {
+  static constexpr int nmax = NMAX, mmax = MMAX;
+  static constexpr Lay L = make_layout(NMAX, MMAX);
 };
 
 struct IO {
@@ -69,6 +108,7 @@ struct IO {
   double *x_out, *f_out, *g_out, *lam_x, *lam_g, *X_out;
   int *status, *iters;
   double* trace;
+  double* ws;  // per-scenario global workspace, B x wstotal
 };
 
 __device__ __forceinline__ double wsum(double v) {
@@ -87,6 +127,11 @@ __device__ __forceinline__ double wmin(double v) {
   return v;
 }
 __device__ __forceinline__ bool wany(bool b) { return __any((int)b) != 0; }
+__device__ __forceinline__ double readlane_d(double v, int l) {
+  const int lo = __builtin_amdgcn_readlane(__double2loint(v), l);
+  const int hi = __builtin_amdgcn_readlane(__double2hiint(v), l);
+  return __hiloint2double(hi, lo);
+}
 // reciprocal / reciprocal square root: hardware estimate + two Newton steps
 // (~1 ulp; the IEEE-exact fp64 division sequence is ~2x longer).  Only used on
 // finite non-zero arguments (slacks, distances, pivots).
@@ -131,48 +176,58 @@ enum Phase { PH_ROLLOUT, PH_EVAL, PH_DERIVS, PH_ADJ, PH_SUMM, PH_RIC, PH_RESOLVE
 #ifdef NMPC_STAMPS
 #define STAMP0() const unsigned long long _ts0 = __builtin_amdgcn_s_memtime()
 #define STAMP1(ph) do { const unsigned long long _ts1 = __builtin_amdgcn_s_memtime(); \
-    if (lane == 0) stamps[ph] += (double)(_ts1 - _ts0); } while (0)
+    if (lanef() == 0) stamps[ph] += (double)(_ts1 - _ts0); } while (0)
 #else
 #define STAMP0() do {} while (0)
 #define STAMP1(ph) do {} while (0)
 #endif
 
+template <class CAP>
 struct Solver {
   const CST Params* __restrict__ P;
   LDS double* sm;
-  int lane, b;
+  int lane_, b;
+  // The lane index is re-materialised behind an empty asm at every use so the
+  // compiler cannot hoist per-lane address arithmetic of every array out of
+  // the main loop (that LICM kept ~200 extra VGPRs live for the whole kernel).
+  __device__ __forceinline__ int lanef() const { int x = lane_; asm volatile("" : "+v"(x)); return x; }
   int N, m, nobs, nw, ng;
   double T;
   // pointers into LDS
-  LDS double* U, *Ut, *dU, *dU2, *zl, *zu, *xl, *xu, *sigx, *ru;
-  LDS double* X, *Xt, *dX, *dX2;
-  LDS double* s, *y, *vl, *vu, *d, *dt, *ds, *ds2, *dc, *dl, *du, *dms;
-  LDS double* gl, *Hl, *trig, *st, *lam;
-  LDS double* K, *kf, *Lc, *Pa, *Pb, *pva, *pvb, *PA, *BtP, *St, *Rt;
-  LDS double* pp, *obx, *oby, *inc, *filt, *stamps;
+  GLB double* U, *Ut, *dU, *dU2, *zl, *zu, *xl, *xu, *sigx, *ru;
+  LDS double* X, *Xt, *dX;
+  GLB double* s, *y, *vl, *vu, *d, *dt, *ds, *ds2, *dc, *dl, *du, *dms;
+  GLB double* gl, *Hl, *Qs;
+  LDS double* trig, *qs, *lam;
+  GLB double* K, *Rk;
+  LDS double* Kc, *kf, *Rc, *Pa, *Pb, *pva, *pvb, *St;
+  LDS double* pp, *obx, *oby, *inc, *stamps;
+  GLB double* filt;
   // uniform scalars
   double df, mu, tau, delta;
   int nfilt;
   int nzx, nzs;
 
-  __device__ __forceinline__ void bind(const Params* prm, double* smem, int lane_, int b_) {
-    P = (const CST Params*)prm; sm = (LDS double*)smem; lane = lane_; b = b_;
+  __device__ __forceinline__ void bind(const Params* prm, double* smem, double* wsp, int lane_, int b_) {
+    constexpr Lay L = CAP::L;
+    P = (const CST Params*)prm; sm = (LDS double*)smem; this->lane_ = lane_; b = b_;
     N = prm->N; m = prm->m; nobs = prm->nobs; nw = prm->nw; ng = prm->ng; T = prm->T;
-    U = sm + prm->U; Ut = sm + prm->Ut; dU = sm + prm->dU; dU2 = sm + prm->dU2;
-    zl = sm + prm->zl; zu = sm + prm->zu; xl = sm + prm->xl; xu = sm + prm->xu;
-    sigx = sm + prm->sigx; ru = sm + prm->ru;
-    X = sm + prm->X; Xt = sm + prm->Xt; dX = sm + prm->dX; dX2 = sm + prm->dX2;
-    s = sm + prm->s; y = sm + prm->y; vl = sm + prm->vl; vu = sm + prm->vu;
-    d = sm + prm->d; dt = sm + prm->dt; ds = sm + prm->ds; ds2 = sm + prm->ds2;
-    dc = sm + prm->dc; dl = sm + prm->dl; du = sm + prm->du; dms = sm + prm->dms;
-    gl = sm + prm->gl; Hl = sm + prm->Hl; trig = sm + prm->trig; st = sm + prm->st;
-    lam = sm + prm->lam;
-    K = sm + prm->K; kf = sm + prm->kf; Lc = sm + prm->Lc;
-    Pa = sm + prm->P0; Pb = sm + prm->P1; pva = sm + prm->pv0; pvb = sm + prm->pv1;
-    PA = sm + prm->PA; BtP = sm + prm->BtP; St = sm + prm->St; Rt = sm + prm->Rt;
-    pp = sm + prm->p; obx = sm + prm->ob; oby = obx + NMPC_MAX_OBS; inc = sm + prm->inc;
-    filt = sm + prm->filt;
-    stamps = sm + prm->red;
+    GLB double* gw = (GLB double*)(wsp + (long long)b_ * L.wstotal);
+    U = gw + L.U; Ut = gw + L.Ut; dU = gw + L.dU; dU2 = gw + L.dU2;
+    zl = gw + L.zl; zu = gw + L.zu; xl = gw + L.xl; xu = gw + L.xu;
+    sigx = gw + L.sigx; ru = gw + L.ru;
+    X = sm + L.X; Xt = sm + L.Xt; dX = sm + L.dX;
+    s = gw + L.s; y = gw + L.y; vl = gw + L.vl; vu = gw + L.vu;
+    d = gw + L.d; dt = gw + L.dt; ds = gw + L.ds; ds2 = gw + L.ds2;
+    dc = gw + L.dc; dl = gw + L.dl; du = gw + L.du; dms = gw + L.dms;
+    gl = gw + L.gl; Hl = gw + L.Hl; trig = sm + L.trig; Qs = gw + L.Qs; qs = sm + L.qs;
+    lam = sm + L.lam;
+    K = gw + L.K; kf = sm + L.kf; Rk = gw + L.Rk; Kc = sm + L.Kc; Rc = sm + L.Rc;
+    Pa = sm + L.P0; Pb = sm + L.P1; pva = sm + L.pv0; pvb = sm + L.pv1;
+    St = sm + L.St;
+    pp = sm + L.p; obx = sm + L.ob; oby = obx + NMPC_MAX_OBS; inc = sm + L.inc;
+    filt = gw + L.filt;
+    stamps = sm + L.red;
   }
 
   __device__ __forceinline__ bool hasl(double v) const { return v > -INFINITY; }
@@ -180,11 +235,11 @@ struct Solver {
 
   // ------------------------------------------------------------------ rollout
   // X[:,0] = p[0:8]; X[:,k+1] = X[:,k] + T f(X[:,k],U[:,k])   (NMPC_TT.py:160-167)
-  // Each lane k sums the increments j<k in order, i.e. bitwise the sequential
+  // Each lanef() k sums the increments j<k in order, i.e. bitwise the sequential
   // recursion; the (x,y,z) increments need theta_j, psi_j, so two passes.
-  __device__ __forceinline__ void rollout(const LDS double* Us, LDS double* Xd) {
+  __device__ __forceinline__ void rollout(const GLB double* Us, LDS double* Xd) {
     STAMP0();
-    const int k = lane;
+    const int k = lanef();
     if (k < N) {
 #pragma unroll
       for (int c = 0; c < 5; ++c) inc[k * 8 + c] = T * Us[k * 6 + 1 + c];
@@ -253,9 +308,9 @@ struct Solver {
   }
 
   // f = sum_k l_k(X) and rows dst[r] = dc[r] * g_r(X) (dc may be null -> unscaled)
-  __device__ __forceinline__ double eval_fg(const LDS double* Xs, LDS double* dst, const LDS double* scale) {
+  __device__ __forceinline__ double eval_fg(const LDS double* Xs, GLB double* dst, const GLB double* scale) {
     STAMP0();
-    const int k = lane;
+    const int k = lanef();
     double f = 0.0;
     if (k <= N) {
       const LDS double* xk = Xs + k * 8;
@@ -272,20 +327,20 @@ struct Solver {
     return fs;
   }
 
-  // --------------------------------------------- stage derivatives at X (lane=k)
+  // --------------------------------------------- stage derivatives at X (lanef()=k)
   // gl[k] = grad l_k (8), Hl[k] = hess l_k packed over (x,y,z,x5,x6,x7), trig[k].
   // Derivation: oracle/nmpc_oracle.py::stage_cost_derivs (Q = (r1/a)^2+(r2/b)^2).
-  __device__ __forceinline__ void derivs(const LDS double* Xs, const LDS double* Us) {
+  __device__ __forceinline__ void derivs(const LDS double* Xs, const GLB double* Us) {
     STAMP0();
-    const int k = lane;
+    const int k = lanef();
     if (k <= N) {
       const LDS double* xk = Xs + k * 8;
       const double th = xk[3], ps = xk[4];
       LDS double* tg = trig + k * 8;
       tg[0] = cos(th); tg[1] = sin(th); tg[2] = cos(ps); tg[3] = sin(ps);
       tg[4] = (k < N) ? Us[k * 6] : 0.0;
-      LDS double* g8 = gl + k * 8;
-      LDS double* H = Hl + k * 21;
+      GLB double* g8 = gl + k * 8;
+      GLB double* H = Hl + k * 21;
       if (k == N) {
         for (int i = 0; i < 8; ++i) g8[i] = 0.0;
         for (int i = 0; i < 21; ++i) H[i] = 0.0;
@@ -379,12 +434,12 @@ struct Solver {
     b00 = T * cp * ct; b10 = T * sp * ct; b20 = T * stt;
   }
 
-  // --------------------------------------------- adjoint lam_k (lane = k)
+  // --------------------------------------------- adjoint lam_k (lanef() = k)
   // lam_N = G_N^T y_N; lam_k = ofac*gl_k + G_k^T y_k + A_k^T lam_{k+1}
   // (oracle SSEval.hessian).  yy may be null (objective only).
-  __device__ __forceinline__ void adjoint(double ofac, const LDS double* yy) {
+  __device__ __forceinline__ void adjoint(double ofac, const GLB double* yy) {
     STAMP0();
-    const int k = lane;
+    const int k = lanef();
     LDS double* wv = inc;  // scratch 8*(N+1)
     if (k <= N) {
       double w[8];
@@ -453,18 +508,18 @@ struct Solver {
   __device__ __forceinline__ double su_x(int i, const LDS double* u) const { return xu[i] - u[i]; }
 
   // barrier objective phi (oracle barrier_obj) at (u, s + a*ds) [sv == null -> s]
-  __device__ __forceinline__ double barrier_obj(double f, const LDS double* u, const LDS double* sb, const LDS double* dsv,
+  __device__ __forceinline__ double barrier_obj(double f, const GLB double* u, const GLB double* sb, const GLB double* dsv,
                                 double a) const {
     STAMP0();
     double logs = 0.0, damp = 0.0;
-    for (int i = lane; i < nw; i += WAVE) {
+    for (int i = lanef(); i < nw; i += WAVE) {
       const bool lo = hasl(xl[i]), hi = hasu(xu[i]);
       if (lo) logs += log(u[i] - xl[i]);
       if (hi) logs += log(xu[i] - u[i]);
       if (lo && !hi) damp += u[i] - xl[i];
       if (hi && !lo) damp += xu[i] - u[i];
     }
-    for (int r = lane; r < ng; r += WAVE) {
+    for (int r = lanef(); r < ng; r += WAVE) {
       const double sv = dsv ? sb[r] + a * dsv[r] : sb[r];
       const bool lo = hasl(dl[r]), hi = hasu(du[r]);
       if (lo) logs += log(sv - dl[r]);
@@ -479,15 +534,16 @@ struct Solver {
     return rr;
   }
 
-  // -------------------------------------------- Riccati: per-stage summaries
-  // st[k] = {Qxy(3), Qbox(5), qxy(2), qbox(5)}: contributions of the stage-k
-  // rows to the stage Hessian / gradient.  Modes:
-  //  NEWTON: Q += Gt^T D Gt + sum_obs y dc Hg ; q += Gt^T (y + D rd + rs)
-  //  SOC:    q only, with rd := dms
-  //  LS:     Q += Gt^T Gt ; q += -Gt^T (vu - vl)           (least-squares y init)
-  __device__ __forceinline__ void summaries(int mode) {
+  // -------------------------------------------- Riccati: stage assembly
+  // Stage-parallel (lanef() = stage k) assembly of the LQ subproblem:
+  //   Qs[k] = Q_k (8x8 symmetric, packed upper, 36), qs[k] = {q_k (8), S_k[0][3], S_k[0][4]}.
+  //  NEWTON: Q = hfac*Hl + Gt^T D Gt + sum_obs y dc Hg + dyn(lam_{k+1}) ; q = gfac*gl + Gt^T (y + D rd + rs)
+  //  SOC:    q only, with rd := dms (Q, S unchanged)
+  //  LS:     Q = Gt^T Gt ; q = gfac*gl - Gt^T (vu - vl)   (least-squares y init, gfac = -df)
+  __device__ __forceinline__ static int pk8(int i, int j) { return i * (15 - i) / 2 + j; }  // i <= j
+  __device__ __forceinline__ void assemble(int mode, double hfac, double gfac, bool dyn) {
     STAMP0();
-    const int k = lane;
+    const int k = lanef();
     if (k <= N) {
       const LDS double* xk = X + k * 8;
       double Qxy0 = 0, Qxy1 = 0, Qxy2 = 0, qx = 0, qy = 0;
@@ -502,8 +558,7 @@ struct Solver {
         } else {
           const bool lo = hasl(dl[r]), hi = hasu(du[r]);
           const double iSl = lo ? rcp(s[r] - dl[r]) : 0.0, iSu = hi ? rcp(du[r] - s[r]) : 0.0;
-          const double sig = vl[r] * iSl + vu[r] * iSu;
-          const double D = sig + delta;
+          const double D = vl[r] * iSl + vu[r] * iSu + delta;
           const double rs = -y[r] - mu * iSl + mu * iSu +
                             kd * mu * ((lo && !hi ? 1.0 : 0.0) - (hi && !lo ? 1.0 : 0.0));
           const double rd = (mode == SUM_SOC) ? dms[r] : d[r] - s[r];
@@ -528,138 +583,136 @@ struct Solver {
           qy += dc[r] * Bw * gy;
         }
       }
-      LDS double* o16 = st + k * 16;
-      o16[0] = Qxy0; o16[1] = Qxy1; o16[2] = Qxy2;
+      LDS double* qo = qs + k * 10;
+      qo[0] = gfac * gl[k * 8 + 0] + qx;
+      qo[1] = gfac * gl[k * 8 + 1] + qy;
+      qo[2] = gfac * gl[k * 8 + 2] + qb[0];
+      qo[3] = gfac * gl[k * 8 + 3] + qb[1];
+      qo[4] = gfac * gl[k * 8 + 4];
+      qo[5] = gfac * gl[k * 8 + 5] + qb[2];
+      qo[6] = gfac * gl[k * 8 + 6] + qb[3];
+      qo[7] = gfac * gl[k * 8 + 7] + qb[4];
+      if (mode != SUM_SOC) {
+        double Q[36];
 #pragma unroll
-      for (int i = 0; i < 5; ++i) { o16[3 + i] = Qb[i]; o16[10 + i] = qb[i]; }
-      o16[8] = qx; o16[9] = qy;
+        for (int t = 0; t < 36; ++t) Q[t] = 0.0;
+        if (hfac != 0.0) {
+          const int sv[6] = {0, 1, 2, 5, 6, 7};
+#pragma unroll
+          for (int a = 0; a < 6; ++a) {
+#pragma unroll
+            for (int bq = a; bq < 6; ++bq) Q[pk8(sv[a], sv[bq])] += hfac * Hl[k * 21 + hp(a, bq)];
+          }
+        }
+        Q[pk8(0, 0)] += Qxy0; Q[pk8(0, 1)] += Qxy1; Q[pk8(1, 1)] += Qxy2;
+        Q[pk8(2, 2)] += Qb[0]; Q[pk8(3, 3)] += Qb[1]; Q[pk8(5, 5)] += Qb[2];
+        Q[pk8(6, 6)] += Qb[3]; Q[pk8(7, 7)] += Qb[4];
+        double s03 = 0.0, s04 = 0.0;
+        if (dyn && k < N) {
+          const LDS double* tg = trig + k * 8;
+          const double ct = tg[0], stt = tg[1], cp = tg[2], sp = tg[3], v = tg[4];
+          const LDS double* ln = lam + (k + 1) * 8;
+          const double l0 = ln[0], l1 = ln[1], l2 = ln[2];
+          Q[pk8(3, 3)] += T * (-l0 * v * cp * ct - l1 * v * sp * ct - l2 * v * stt);
+          Q[pk8(4, 4)] += T * (-l0 * v * cp * ct - l1 * v * sp * ct);
+          Q[pk8(3, 4)] += T * (l0 * v * sp * stt - l1 * v * cp * stt);
+          s03 = T * (-l0 * cp * stt - l1 * sp * stt + l2 * ct);
+          s04 = T * (-l0 * sp * ct + l1 * cp * ct);
+        }
+#pragma unroll
+        for (int t = 0; t < 36; ++t) Qs[k * 36 + t] = Q[t];
+        qo[8] = s03;
+        qo[9] = s04;
+      }
     }
-    STAMP1(PH_SUMM);
     sync();
-  }
-
-  // stage Hessian entry Q_k[i][j] (hfac*Hl + rows + dynamics with lam_{k+1})
-  __device__ __forceinline__ double Qentry(int k, int i, int j, double hfac, bool dyn) const {
-    double q = 0.0;
-    const int vi = vloc(i), vj = vloc(j);
-    if (vi >= 0 && vj >= 0) q += hfac * Hl[k * 21 + hp(vi, vj)];
-    const LDS double* o16 = st + k * 16;
-    if (i < 2 && j < 2) q += o16[i + j];  // Qxy0 (0,0), Qxy1 (0,1)/(1,0), Qxy2 (1,1)
-    if (i == j) {
-      if (i == 2) q += o16[3];
-      else if (i == 3) q += o16[4];
-      else if (i >= 5) q += o16[i + 0];  // 5->o16[5], 6->o16[6], 7->o16[7]
-    }
-    if (dyn && k < N && (i == 3 || i == 4) && (j == 3 || j == 4)) {
-      const LDS double* tg = trig + k * 8;
-      const double ct = tg[0], stt = tg[1], cp = tg[2], sp = tg[3], v = tg[4];
-      const LDS double* ln = lam + (k + 1) * 8;
-      const double l0 = ln[0], l1 = ln[1], l2 = ln[2];
-      if (i == 3 && j == 3) q += T * (-l0 * v * cp * ct - l1 * v * sp * ct - l2 * v * stt);
-      else if (i == 4 && j == 4) q += T * (-l0 * v * cp * ct - l1 * v * sp * ct);
-      else q += T * (l0 * v * sp * stt - l1 * v * cp * stt);
-    }
-    return q;
-  }
-  __device__ __forceinline__ double qentry(int k, int i, double gfac) const {
-    double q = gfac * gl[k * 8 + i];
-    const LDS double* o16 = st + k * 16;
-    if (i == 0) q += o16[8];
-    else if (i == 1) q += o16[9];
-    else if (i == 2) q += o16[10];
-    else if (i == 3) q += o16[11];
-    else if (i >= 5) q += o16[7 + i];  // 5->12, 6->13, 7->14
-    return q;
-  }
-  // S_k[0][3], S_k[0][4] (dynamics cross terms, oracle dyn_hess Hxu)
-  __device__ __forceinline__ void Sdyn(int k, double& s03, double& s04) const {
-    const LDS double* tg = trig + k * 8;
-    const double ct = tg[0], stt = tg[1], cp = tg[2], sp = tg[3];
-    const LDS double* ln = lam + (k + 1) * 8;
-    const double l0 = ln[0], l1 = ln[1], l2 = ln[2];
-    s03 = T * (-l0 * cp * stt - l1 * sp * stt + l2 * ct);
-    s04 = T * (-l0 * sp * ct + l1 * cp * ct);
+    STAMP1(PH_SUMM);
   }
 
   // ----------------------------------------- Riccati factorisation + solve
-  // Backward sweep over stages with lane (i,j) owning entry (i,j) of the 8x8
-  // cost-to-go matrix.  Returns false if a pivot of some R~_k is not positive
-  // (wrong inertia).  Stores K_k, k_k, chol(R~_k) for the forward sweep / SOC.
-  //   hfac, gfac: factors on the stage cost Hessian / gradient; dyn: add the
-  //   dynamics second derivatives; Rd: diag of R (null -> 1).
-  __device__ __forceinline__ bool riccati(double hfac, double gfac, bool dyn, const LDS double* Rd, const LDS double* rv) {
+  // Backward sweep over stages, lanef() (i,j) owning entry (i,j) of the 8x8
+  // cost-to-go matrix, three LDS exchanges per stage:
+  //   (1) A^T P A (register), S~ = S + B^T P A and R~ = R + B^T P B (21 lanes)
+  //       straight from P (A = I + E, B = [b0 | T e_3..7]);
+  //   (2) every lanef(): Cholesky of R~ (inertia: all pivots > 0), R~^{-1};
+  //       lanes 0..7: column j of K = -R~^{-1} S~, lanef() 8: k = -R~^{-1} r~;
+  //   (3) P_k = Q_k + A^T P A + S~^T K ; p_k = q_k + A^T p + K^T r~.
+  // Stores K_k, k_k and R~_k (for the gradient-only re-solve).
+  __device__ __forceinline__ bool riccati(const GLB double* Rd, const GLB double* rv) {
+#ifdef NMPC_STAMPS
+    if (lanef() == 0) stamps[PH_RB] += 1.0;  // count factorisations
+#endif
     STAMP0();
-    const bool r = riccati_(hfac, gfac, dyn, Rd, rv);
+    const bool r = riccati_(Rd, rv);
     STAMP1(PH_RIC);
     return r;
   }
-  __device__ __forceinline__ bool riccati_(double hfac, double gfac, bool dyn, const LDS double* Rd, const LDS double* rv) {
-    const int i = lane >> 3, j = lane & 7;
+  __device__ __forceinline__ bool riccati_(const GLB double* Rd, const GLB double* rv) {
+    const int i = lanef() >> 3, j = lanef() & 7;
+    const int ij = (i <= j) ? pk8(i, j) : pk8(j, i);
     LDS double* Pc = Pa;
     LDS double* Pn = Pb;
     LDS double* pc = pva;
     LDS double* pn = pvb;
-    Pc[lane] = Qentry(N, i, j, hfac, dyn);
-    if (lane < 8) pc[lane] = qentry(N, lane, gfac);
+    Pc[lanef()] = Qs[N * 36 + ij];
+    if (lanef() < 8) pc[lanef()] = qs[N * 10 + lanef()];
+    // lanes 48..63 -> R~ entries t = 0..15, lanes 0..4 -> t = 16..20 (packed lower)
+    const int tR = lanef() >= 48 ? lanef() - 48 : (lanef() < 5 ? 16 + lanef() : -1);
+    int rR = 0;
+    while (tR >= 0 && (rR + 1) * (rR + 2) / 2 <= tR) ++rR;
+    const int cR = tR >= 0 ? tR - rR * (rR + 1) / 2 : 0;
+    const int rowS = (i >= 1 && i < 6) ? 2 + i : 3;
     sync();
     bool ok = true;
     for (int k = N - 1; k >= 0; --k) {
       double E03, E04, E13, E14, E23, b00, b10, b20;
       stage_AB(k, E03, E04, E13, E14, E23, b00, b10, b20);
-      // (A) PA = P A ; BtP = B^T P
-      { STAMP0();
-      {
-        const LDS double* Pi = Pc + i * 8;
-        double v = Pi[j];
-        if (j == 3) v = v + ((Pi[0] * E03 + Pi[1] * E13) + Pi[2] * E23);
-        else if (j == 4) v = v + (Pi[0] * E04 + Pi[1] * E14);
-        PA[lane] = v;
-        if (lane < 48) {
-          const int r = i, jj = j;
-          BtP[lane] = (r == 0) ? ((b00 * Pc[jj] + b10 * Pc[8 + jj]) + b20 * Pc[16 + jj])
-                               : T * Pc[(2 + r) * 8 + jj];
-        }
-      }
-      sync();
-      STAMP1(PH_RA); }
-      // (B) APA = A^T P A (register) ; St = S + B^T P A
+      const double aj0 = (j == 3) ? E03 : (j == 4 ? E04 : 0.0);
+      const double aj1 = (j == 3) ? E13 : (j == 4 ? E14 : 0.0);
+      const double aj2 = (j == 3) ? E23 : 0.0;
+      const double ai0 = (i == 3) ? E03 : (i == 4 ? E04 : 0.0);
+      const double ai1 = (i == 3) ? E13 : (i == 4 ? E14 : 0.0);
+      const double ai2 = (i == 3) ? E23 : 0.0;
+      const double qv = Qs[k * 36 + ij];  // global, issued early
       double APA;
+      // ---- (1)
       { STAMP0();
-      {
-        double v = PA[lane];
-        if (i == 3) v = v + ((E03 * PA[j] + E13 * PA[8 + j]) + E23 * PA[16 + j]);
-        else if (i == 4) v = v + (E04 * PA[j] + E14 * PA[8 + j]);
-        APA = v;
-        if (lane < 48) {
-          const int r = i, jj = j;
-          double sv = (r == 0) ? ((b00 * PA[jj] + b10 * PA[8 + jj]) + b20 * PA[16 + jj])
-                               : T * PA[(2 + r) * 8 + jj];
-          if (dyn && r == 0 && (jj == 3 || jj == 4)) {
-            double s03, s04;
-            Sdyn(k, s03, s04);
-            sv += (jj == 3) ? s03 : s04;
+        const double P00 = Pc[0], P01 = Pc[1], P02 = Pc[2], P11 = Pc[9], P12 = Pc[10], P22 = Pc[18];
+        const double P0j = Pc[j], P1j = Pc[8 + j], P2j = Pc[16 + j];
+        const double Pi0 = Pc[i * 8], Pi1 = Pc[i * 8 + 1], Pi2 = Pc[i * 8 + 2], Pij = Pc[lanef()];
+        const double PA0j = P0j + ((P00 * aj0 + P01 * aj1) + P02 * aj2);
+        const double PA1j = P1j + ((P01 * aj0 + P11 * aj1) + P12 * aj2);
+        const double PA2j = P2j + ((P02 * aj0 + P12 * aj1) + P22 * aj2);
+        const double PAij = Pij + ((Pi0 * aj0 + Pi1 * aj1) + Pi2 * aj2);
+        APA = PAij + ((ai0 * PA0j + ai1 * PA1j) + ai2 * PA2j);
+        const double Prj = Pc[rowS * 8 + j], Pr0 = Pc[rowS * 8], Pr1 = Pc[rowS * 8 + 1], Pr2 = Pc[rowS * 8 + 2];
+        const double PArj = Prj + ((Pr0 * aj0 + Pr1 * aj1) + Pr2 * aj2);
+        double stv = (i == 0) ? ((b00 * PA0j + b10 * PA1j) + b20 * PA2j) : T * PArj;
+        stv += (i == 0 && j == 3) ? qs[k * 10 + 8] : ((i == 0 && j == 4) ? qs[k * 10 + 9] : 0.0);
+        if (lanef() < 48) St[lanef()] = stv;
+        if (tR >= 0) {
+          double v;
+          if (rR == 0) {  // b0^T P[0:3,0:3] b0
+            v = b00 * ((P00 * b00 + P01 * b10) + P02 * b20) + b10 * ((P01 * b00 + P11 * b10) + P12 * b20) +
+                b20 * ((P02 * b00 + P12 * b10) + P22 * b20);
+          } else if (cR == 0) {
+            const LDS double* Pr = Pc + (2 + rR) * 8;
+            v = T * ((Pr[0] * b00 + Pr[1] * b10) + Pr[2] * b20);
+          } else {
+            v = T * (T * Pc[(2 + rR) * 8 + 2 + cR]);
           }
-          St[lane] = sv;
+          if (rR == cR) v += (Rd ? Rd[k * 6 + rR] : 1.0) + delta;
+          Rc[tR] = v;
+          Rk[k * 21 + tR] = v;
         }
-        if (lane >= 48 || lane < 5) {  // 21 lanes build R~ = R + B^T P B (packed lower)
-          const int t = lane >= 48 ? lane - 48 : 16 + lane;
-          int r = 0;
-          while ((r + 1) * (r + 2) / 2 <= t) ++r;
-          const int c = t - r * (r + 1) / 2;
-          double v = (c == 0) ? ((BtP[r * 8 + 0] * b00 + BtP[r * 8 + 1] * b10) + BtP[r * 8 + 2] * b20)
-                              : T * BtP[r * 8 + 2 + c];
-          if (r == c) v += (Rd ? Rd[k * 6 + r] : 1.0) + delta;
-          Rt[t] = v;
-        }
-      }
-      sync();
-      STAMP1(PH_RB); }
-      // (C) every lane: Cholesky of R~ (pivots by rsqrt), r~ = r + B^T p
-      STAMP0();
-      double Lm[21], idg[6], rt[6];
-      {
+        sync();
+        STAMP1(PH_RA); }
+      // ---- (2)
+      double rt[6];
+      { STAMP0();
+        double Lm[21], idg[6];
 #pragma unroll
-        for (int t = 0; t < 21; ++t) Lm[t] = Rt[t];
+        for (int t = 0; t < 21; ++t) Lm[t] = Rc[t];
 #pragma unroll
         for (int c = 0; c < 6; ++c) {
           double dg = Lm[c * (c + 1) / 2 + c];
@@ -677,92 +730,104 @@ struct Solver {
             Lm[r * (r + 1) / 2 + c] = v * ig;
           }
         }
-        // r~ = r_k + B^T p_{k+1}
+        // L^{-1} (packed lower) and R~^{-1} = L^{-T} L^{-1} (packed lower)
+        double Li[21], Rv[21];
+#pragma unroll
+        for (int c = 0; c < 6; ++c) {
+          Li[c * (c + 1) / 2 + c] = idg[c];
+#pragma unroll
+          for (int r = c + 1; r < 6; ++r) {
+            double a = 0.0;
+#pragma unroll
+            for (int t = c; t < r; ++t) a += Lm[r * (r + 1) / 2 + t] * Li[t * (t + 1) / 2 + c];
+            Li[r * (r + 1) / 2 + c] = -idg[r] * a;
+          }
+        }
+#pragma unroll
+        for (int r = 0; r < 6; ++r) {
+#pragma unroll
+          for (int c = 0; c <= r; ++c) {
+            double a = 0.0;
+#pragma unroll
+            for (int t = r; t < 6; ++t) a += Li[t * (t + 1) / 2 + r] * Li[t * (t + 1) / 2 + c];
+            Rv[r * (r + 1) / 2 + c] = a;
+          }
+        }
         rt[0] = rv[k * 6 + 0] + ((b00 * pc[0] + b10 * pc[1]) + b20 * pc[2]);
 #pragma unroll
         for (int r = 1; r < 6; ++r) rt[r] = rv[k * 6 + r] + T * pc[2 + r];
-      }
-      STAMP1(PH_RC);
-      ok = !wany(!ok);  // every lane computed the same pivots; make it explicit
-      if (!ok) break;
-      // (D) K = -R~^{-1} St (lanes 0..7 one column each), kf = -R~^{-1} r~
-      { STAMP0();
-      {
-        if (lane < 9) {
-          double v[6];
+        if (lanef() < 9) {
+          double col[6];
 #pragma unroll
-          for (int r = 0; r < 6; ++r) v[r] = (lane < 8) ? St[r * 8 + lane] : rt[r];
-          // forward L z = v
+          for (int r = 0; r < 6; ++r) col[r] = (lanef() < 8) ? St[r * 8 + lanef()] : rt[r];
 #pragma unroll
           for (int r = 0; r < 6; ++r) {
-            double a = v[r];
+            double a = 0.0;
 #pragma unroll
-            for (int t = 0; t < r; ++t) a -= Lm[r * (r + 1) / 2 + t] * v[t];
-            v[r] = a * idg[r];
-          }
-          // backward L^T x = z
-#pragma unroll
-          for (int r = 5; r >= 0; --r) {
-            double a = v[r];
-#pragma unroll
-            for (int t = r + 1; t < 6; ++t) a -= Lm[t * (t + 1) / 2 + r] * v[t];
-            v[r] = a * idg[r];
-          }
-          if (lane < 8) {
-#pragma unroll
-            for (int r = 0; r < 6; ++r) K[k * 48 + r * 8 + lane] = -v[r];
-          } else {
-#pragma unroll
-            for (int r = 0; r < 6; ++r) kf[k * 6 + r] = -v[r];
+            for (int c = 0; c < 6; ++c) a += Rv[r >= c ? r * (r + 1) / 2 + c : c * (c + 1) / 2 + r] * col[c];
+            if (lanef() < 8) { Kc[r * 8 + lanef()] = -a; K[k * 48 + r * 8 + lanef()] = -a; }
+            else kf[k * 6 + r] = -a;
           }
         }
-        if (lane == 9) {
-          LDS double* lc = Lc + k * 28;
-#pragma unroll
-          for (int t = 0; t < 21; ++t) lc[t] = Lm[t];
-#pragma unroll
-          for (int t = 0; t < 6; ++t) lc[21 + t] = idg[t];
-        }
-      }
-      sync();
-      STAMP1(PH_RD); }
-      // (E) P_k = Q_k + A^T P A + St^T K ; p_k = q_k + A^T p + K^T r~
+        sync();
+        STAMP1(PH_RD); }
+      ok = !wany(!ok);  // every lanef() computed the same pivots; make it explicit
+      if (!ok) break;
+      // ---- (3)
       { STAMP0();
-      {
         double sk = 0.0;
 #pragma unroll
-        for (int r = 0; r < 6; ++r) sk += St[r * 8 + i] * K[k * 48 + r * 8 + j];
-        Pn[lane] = (Qentry(k, i, j, hfac, dyn) + APA) + sk;
-        if (lane < 8) {
-          double atp = pc[lane];
-          if (lane == 3) atp = atp + ((E03 * pc[0] + E13 * pc[1]) + E23 * pc[2]);
-          else if (lane == 4) atp = atp + (E04 * pc[0] + E14 * pc[1]);
+        for (int r = 0; r < 6; ++r) sk += St[r * 8 + i] * Kc[r * 8 + j];
+        Pn[lanef()] = (qv + APA) + sk;
+        if (lanef() < 8) {
+          double atp = pc[lanef()];
+          if (lanef() == 3) atp = atp + ((E03 * pc[0] + E13 * pc[1]) + E23 * pc[2]);
+          else if (lanef() == 4) atp = atp + (E04 * pc[0] + E14 * pc[1]);
           double kr = 0.0;
 #pragma unroll
-          for (int r = 0; r < 6; ++r) kr += K[k * 48 + r * 8 + lane] * rt[r];
-          pn[lane] = (qentry(k, lane, gfac) + atp) + kr;
+          for (int r = 0; r < 6; ++r) kr += Kc[r * 8 + lanef()] * rt[r];
+          pn[lanef()] = (qs[k * 10 + lanef()] + atp) + kr;
         }
-      }
-      sync();
-      STAMP1(PH_RE); }
+        sync();
+        STAMP1(PH_RE); }
       LDS double* t1 = Pc; Pc = Pn; Pn = t1;
       LDS double* t2 = pc; pc = pn; pn = t2;
     }
     return ok;
   }
 
-  // gradient-only re-solve with the stored factors (second-order correction)
-  __device__ __forceinline__ void resolve(double gfac, const LDS double* rv) {
+  // gradient-only re-solve with the stored factors (second-order correction):
+  // every lanef() runs the vector recursion redundantly (R~_k re-factorised).
+  __device__ __forceinline__ void resolve(const GLB double* rv) {
+#ifdef NMPC_STAMPS
+    if (lanef() == 0) stamps[PH_RC] += 1.0;  // count SOC re-solves
+#endif
     STAMP0();
-    // every lane runs the vector recursion redundantly (no LDS exchange)
     double p8[8];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) p8[i] = qentry(N, i, gfac);
+    for (int i = 0; i < 8; ++i) p8[i] = qs[N * 10 + i];
     for (int k = N - 1; k >= 0; --k) {
       double E03, E04, E13, E14, E23, b00, b10, b20;
       stage_AB(k, E03, E04, E13, E14, E23, b00, b10, b20);
-      const LDS double* lc = Lc + k * 28;
-      double rt[6], v[6];
+      double Lm[21], idg[6], rt[6], v[6];
+#pragma unroll
+      for (int t = 0; t < 21; ++t) Lm[t] = Rk[k * 21 + t];
+#pragma unroll
+      for (int c = 0; c < 6; ++c) {
+        double dg = Lm[c * (c + 1) / 2 + c];
+#pragma unroll
+        for (int t = 0; t < c; ++t) dg -= Lm[c * (c + 1) / 2 + t] * Lm[c * (c + 1) / 2 + t];
+        const double ig = rsq(dg);
+        Lm[c * (c + 1) / 2 + c] = dg * ig;
+        idg[c] = ig;
+#pragma unroll
+        for (int r = c + 1; r < 6; ++r) {
+          double a = Lm[r * (r + 1) / 2 + c];
+#pragma unroll
+          for (int t = 0; t < c; ++t) a -= Lm[r * (r + 1) / 2 + t] * Lm[c * (c + 1) / 2 + t];
+          Lm[r * (r + 1) / 2 + c] = a * ig;
+        }
+      }
       rt[0] = rv[k * 6 + 0] + ((b00 * p8[0] + b10 * p8[1]) + b20 * p8[2]);
 #pragma unroll
       for (int r = 1; r < 6; ++r) rt[r] = rv[k * 6 + r] + T * p8[2 + r];
@@ -770,17 +835,17 @@ struct Solver {
       for (int r = 0; r < 6; ++r) {
         double a = rt[r];
 #pragma unroll
-        for (int t = 0; t < r; ++t) a -= lc[r * (r + 1) / 2 + t] * v[t];
-        v[r] = a * lc[21 + r];
+        for (int t = 0; t < r; ++t) a -= Lm[r * (r + 1) / 2 + t] * v[t];
+        v[r] = a * idg[r];
       }
 #pragma unroll
       for (int r = 5; r >= 0; --r) {
         double a = v[r];
 #pragma unroll
-        for (int t = r + 1; t < 6; ++t) a -= lc[t * (t + 1) / 2 + r] * v[t];
-        v[r] = a * lc[21 + r];
+        for (int t = r + 1; t < 6; ++t) a -= Lm[t * (t + 1) / 2 + r] * v[t];
+        v[r] = a * idg[r];
       }
-      if (lane == 0) {
+      if (lanef() == 0) {
 #pragma unroll
         for (int r = 0; r < 6; ++r) kf[k * 6 + r] = -v[r];
       }
@@ -793,57 +858,56 @@ struct Solver {
         double kr = 0.0;
 #pragma unroll
         for (int r = 0; r < 6; ++r) kr += K[k * 48 + r * 8 + i] * rt[r];
-        pn[i] = (qentry(k, i, gfac) + atp) + kr;
+        pn[i] = (qs[k * 10 + i] + atp) + kr;
       }
 #pragma unroll
       for (int i = 0; i < 8; ++i) p8[i] = pn[i];
     }
-    STAMP1(PH_RESOLVE);
     sync();
+    STAMP1(PH_RESOLVE);
   }
 
-  // forward sweep: du_k = K_k dx_k + k_k ; dx_{k+1} = A_k dx_k + B_k du_k
-  // (redundant in every lane, broadcast LDS reads; lane 0 stores)
-  __device__ __forceinline__ void forward(LDS double* dUo, LDS double* dXo) {
+  // forward sweep: du_k = K_k dx_k + k_k ; dx_{k+1} = A_k dx_k + B_k du_k.
+  // Lanes 0..5 form du_k[r] (row r of K); readlane broadcasts it; every lanef()
+  // carries dx redundantly.  Lane 0 stores dX.
+  __device__ __forceinline__ void forward(GLB double* dUo, LDS double* dXo) {
     STAMP0();
     double dx[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) dx[i] = 0.0;
-    if (lane < 8) dXo[lane] = 0.0;
+    if (lanef() < 8) dXo[lanef()] = 0.0;
+    const int r = lanef() < 6 ? lanef() : 5;
     for (int k = 0; k < N; ++k) {
       double E03, E04, E13, E14, E23, b00, b10, b20;
       stage_AB(k, E03, E04, E13, E14, E23, b00, b10, b20);
+      double a = kf[k * 6 + r];
+#pragma unroll
+      for (int c = 0; c < 8; ++c) a += K[k * 48 + r * 8 + c] * dx[c];
+      if (lanef() < 6) dUo[k * 6 + lanef()] = a;
       double du_[6];
 #pragma unroll
-      for (int r = 0; r < 6; ++r) {
-        double a = kf[k * 6 + r];
-#pragma unroll
-        for (int c = 0; c < 8; ++c) a += K[k * 48 + r * 8 + c] * dx[c];
-        du_[r] = a;
-      }
+      for (int q = 0; q < 6; ++q) du_[q] = readlane_d(a, q);
       double xn[8];
       xn[0] = dx[0] + (E03 * dx[3] + E04 * dx[4]) + b00 * du_[0];
       xn[1] = dx[1] + (E13 * dx[3] + E14 * dx[4]) + b10 * du_[0];
       xn[2] = dx[2] + E23 * dx[3] + b20 * du_[0];
 #pragma unroll
       for (int c = 0; c < 5; ++c) xn[3 + c] = dx[3 + c] + T * du_[1 + c];
-      if (lane == 0) {
-#pragma unroll
-        for (int r = 0; r < 6; ++r) dUo[k * 6 + r] = du_[r];
+      if (lanef() == 0) {
 #pragma unroll
         for (int c = 0; c < 8; ++c) dXo[(k + 1) * 8 + c] = xn[c];
       }
 #pragma unroll
       for (int c = 0; c < 8; ++c) dx[c] = xn[c];
     }
-    STAMP1(PH_FWD);
     sync();
+    STAMP1(PH_FWD);
   }
 
   // ds_r = Gt_r dX_k + rd_r (J dU = G Z dU = G dX)
-  __device__ __forceinline__ void row_step(const LDS double* dXs, const LDS double* rdsrc, bool rd_is_dms, LDS double* dso) {
+  __device__ __forceinline__ void row_step(const LDS double* dXs, const GLB double* rdsrc, bool rd_is_dms, GLB double* dso) {
     STAMP0();
-    for (int r = lane; r < ng; r += WAVE) {
+    for (int r = lanef(); r < ng; r += WAVE) {
       const int k = r / m, i = r - k * m;
       const LDS double* xk = X + k * 8;
       const LDS double* dxk = dXs + k * 8;
@@ -864,15 +928,15 @@ struct Solver {
   }
 
   // primal fraction to the boundary (oracle frac_to_bound)
-  __device__ __forceinline__ double frac_to_bound(double tau_, const LDS double* dUs, const LDS double* dss) const {
+  __device__ __forceinline__ double frac_to_bound(double tau_, const GLB double* dUs, const GLB double* dss) const {
     STAMP0();
     double a = 1.0;
-    for (int i = lane; i < nw; i += WAVE) {
+    for (int i = lanef(); i < nw; i += WAVE) {
       const double dx = dUs[i];
       if (hasl(xl[i]) && dx < 0) a = fmin(a, (-tau_ * (U[i] - xl[i])) / dx);
       if (hasu(xu[i]) && -dx < 0) a = fmin(a, (-tau_ * (xu[i] - U[i])) / (-dx));
     }
-    for (int r = lane; r < ng; r += WAVE) {
+    for (int r = lanef(); r < ng; r += WAVE) {
       const double dd = dss[r];
       if (hasl(dl[r]) && dd < 0) a = fmin(a, (-tau_ * (s[r] - dl[r])) / dd);
       if (hasu(du[r]) && -dd < 0) a = fmin(a, (-tau_ * (du[r] - s[r])) / (-dd));
@@ -893,16 +957,16 @@ struct Solver {
     if (hasl(dl[r])) { const double iS = rcp(s[r] - dl[r]); dvl = mu * iS - vl[r] - vl[r] * iS * dsv; }
     if (hasu(du[r])) { const double iS = rcp(du[r] - s[r]); dvu = mu * iS - vu[r] + vu[r] * iS * dsv; }
   }
-  __device__ __forceinline__ double dual_frac_to_bound(double tau_, const LDS double* dUs, const LDS double* dss) const {
+  __device__ __forceinline__ double dual_frac_to_bound(double tau_, const GLB double* dUs, const GLB double* dss) const {
     STAMP0();
     double a = 1.0;
-    for (int i = lane; i < nw; i += WAVE) {
+    for (int i = lanef(); i < nw; i += WAVE) {
       double a1, a2;
       dz_x(i, dUs[i], a1, a2);
       if (hasl(xl[i]) && a1 < 0) a = fmin(a, (-tau_ * zl[i]) / a1);
       if (hasu(xu[i]) && a2 < 0) a = fmin(a, (-tau_ * zu[i]) / a2);
     }
-    for (int r = lane; r < ng; r += WAVE) {
+    for (int r = lanef(); r < ng; r += WAVE) {
       double a1, a2;
       dv_s(r, dss[r], a1, a2);
       if (hasl(dl[r]) && a1 < 0) a = fmin(a, (-tau_ * vl[r]) / a1);
@@ -925,11 +989,11 @@ struct Solver {
   // complementarity max |S z - mu_| over all bounds
   __device__ __forceinline__ double compl_max(double mu_) const {
     double c = 0.0;
-    for (int i = lane; i < nw; i += WAVE) {
+    for (int i = lanef(); i < nw; i += WAVE) {
       if (hasl(xl[i])) c = fmax(c, fabs((U[i] - xl[i]) * zl[i] - mu_));
       if (hasu(xu[i])) c = fmax(c, fabs((xu[i] - U[i]) * zu[i] - mu_));
     }
-    for (int r = lane; r < ng; r += WAVE) {
+    for (int r = lanef(); r < ng; r += WAVE) {
       if (hasl(dl[r])) c = fmax(c, fabs((s[r] - dl[r]) * vl[r] - mu_));
       if (hasu(du[r])) c = fmax(c, fabs((du[r] - s[r]) * vu[r] - mu_));
     }
@@ -939,7 +1003,7 @@ struct Solver {
   // filter
   __device__ __forceinline__ bool filter_ok(double phi, double th) const {
     bool ok = true;
-    for (int e = lane; e < nfilt; e += WAVE) {
+    for (int e = lanef(); e < nfilt; e += WAVE) {
       if (!(phi <= filt[2 * e] || th <= filt[2 * e + 1])) ok = false;
     }
     return !wany(!ok);
@@ -947,7 +1011,7 @@ struct Solver {
   __device__ __forceinline__ void filter_add(double phi, double th) {
     // drop entries dominated by the new one, then append (IpFilter::AddEntry)
     sync();
-    if (lane == 0) {
+    if (lanef() == 0) {
       int w = 0;
       for (int e = 0; e < nfilt; ++e) {
         const double fp = filt[2 * e], ft = filt[2 * e + 1];
@@ -968,15 +1032,15 @@ struct Solver {
 
   // trial point u = U + a dUs, s = s + a dss: rollout into Xt, rows into dt.
   // returns false on an evaluation error (NaN/Inf)
-  __device__ __forceinline__ bool trial(double a, const LDS double* dUs, const LDS double* dss, double& ft, double& phit,
+  __device__ __forceinline__ bool trial(double a, const GLB double* dUs, const GLB double* dss, double& ft, double& phit,
                         double& tht) {
-    for (int i = lane; i < nw; i += WAVE) Ut[i] = U[i] + a * dUs[i];
+    for (int i = lanef(); i < nw; i += WAVE) Ut[i] = U[i] + a * dUs[i];
     sync();
     rollout(Ut, Xt);
     ft = df * eval_fg(Xt, dt, dc);
     double th = 0.0;
     bool bad = false;
-    for (int r = lane; r < ng; r += WAVE) {
+    for (int r = lanef(); r < ng; r += WAVE) {
       const double sv = s[r] + a * dss[r];
       th += fabs(dt[r] - sv);
       if (!isfinite(dt[r])) bad = true;
@@ -990,15 +1054,18 @@ struct Solver {
 };
 
 // ------------------------------------------------------------------ kernel
-__global__ __launch_bounds__(WAVE) void nmpc_solve_kernel(const Params* __restrict__ prm, int B, IO io) {
+template <class CAP>
+__global__ __launch_bounds__(WAVE, 2) void nmpc_solve_kernel(const Params* __restrict__ prm, int B, IO io) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   const int b = blockIdx.x;
   if (b >= B) return;
   const int lane = threadIdx.x;
-  Solver S;
-  S.bind(prm, smem, lane, b);
+  Solver<CAP> S;
+  S.bind(prm, smem, io.ws, lane, b);
+  auto lanef = [&]() { return S.lanef(); };  // for the STAMP macros
+  (void)lanef;
   LDS double* stamps = S.stamps;
-  if (lane < PH_COUNT) stamps[lane] = 0.0;
+  if (S.lanef() < PH_COUNT) stamps[S.lanef()] = 0.0;
   const unsigned long long _tk0 = __builtin_amdgcn_s_memtime();
   (void)_tk0;
   const nmpc_options& o = prm->o;
@@ -1007,29 +1074,29 @@ __global__ __launch_bounds__(WAVE) void nmpc_solve_kernel(const Params* __restri
   double* trace = io.trace ? io.trace + (long long)b * (max_iter + 3) * TRACE_F : nullptr;
 
   // ---------------- load scenario data
-  for (int i = lane; i < prm->np; i += WAVE) S.pp[i] = io.p[(long long)b * io.ld_p + i];
+  for (int i = S.lanef(); i < prm->np; i += WAVE) S.pp[i] = io.p[(long long)b * io.ld_p + i];
   sync();
-  if (lane < S.nobs) {
-    S.obx[lane] = prm->oxp[lane] >= 0 ? S.pp[prm->oxp[lane]] : prm->ox[lane];
-    S.oby[lane] = prm->oyp[lane] >= 0 ? S.pp[prm->oyp[lane]] : prm->oy[lane];
+  if (S.lanef() < S.nobs) {
+    S.obx[S.lanef()] = prm->oxp[S.lanef()] >= 0 ? S.pp[prm->oxp[S.lanef()]] : prm->ox[S.lanef()];
+    S.oby[S.lanef()] = prm->oyp[S.lanef()] >= 0 ? S.pp[prm->oyp[S.lanef()]] : prm->oy[S.lanef()];
   }
   const double brf = o.bound_relax_factor, cvt = o.constr_viol_tol;
   bool invalid = false;
-  for (int i = lane; i < nw; i += WAVE) {
+  for (int i = S.lanef(); i < nw; i += WAVE) {
     S.U[i] = io.x0[(long long)b * io.ld_x0 + i];
     const double lo = io.lbx[(long long)b * io.ld_lbx + i], hi = io.ubx[(long long)b * io.ld_ubx + i];
     S.xl[i] = lo > -BIGB ? lo - fmin(cvt, brf * fmax(1.0, fabs(lo))) : -INFINITY;
     S.xu[i] = hi < BIGB ? hi + fmin(cvt, brf * fmax(1.0, fabs(hi))) : INFINITY;
     if (lo > hi) invalid = true;
   }
-  for (int r = lane; r < ng; r += WAVE) {
+  for (int r = S.lanef(); r < ng; r += WAVE) {
     const double lo = io.lbg[(long long)b * io.ld_lbg + r], hi = io.ubg[(long long)b * io.ld_ubg + r];
     S.dl[r] = lo > -BIGB ? lo - fmin(cvt, brf * fmax(1.0, fabs(lo))) : -INFINITY;  // unscaled for now
     S.du[r] = hi < BIGB ? hi + fmin(cvt, brf * fmax(1.0, fabs(hi))) : INFINITY;
     if (lo >= hi && lo > -BIGB) invalid = true;  // equality rows not supported
     S.dc[r] = 1.0;
   }
-  if (lane == 0) S.filt[2 * FCAP] = 0.0;
+  if (S.lanef() == 0) S.filt[2 * FCAP] = 0.0;
   sync();
   S.nfilt = 0;
   S.delta = 0.0;
@@ -1048,12 +1115,12 @@ __global__ __launch_bounds__(WAVE) void nmpc_solve_kernel(const Params* __restri
     S.adjoint(1.0, nullptr);
     double gmax = 0.0;
     bool bad = !isfinite(F0);
-    for (int i = lane; i < nw; i += WAVE) {
+    for (int i = S.lanef(); i < nw; i += WAVE) {
       const double g = S.grad_u(i);
       if (!isfinite(g)) bad = true;
       gmax = fmax(gmax, fabs(g));
     }
-    for (int r = lane; r < ng; r += WAVE)
+    for (int r = S.lanef(); r < ng; r += WAVE)
       if (!isfinite(S.d[r])) bad = true;
     gmax = wmax(gmax);
     if (wany(bad)) status = ST_INVALID_NUMBER;
@@ -1062,7 +1129,7 @@ __global__ __launch_bounds__(WAVE) void nmpc_solve_kernel(const Params* __restri
     S.df = fmax(dfv, o.nlp_scaling_min_value);
     // Jacobian row maxima: J rows = G_k Z_k, Z_k[:,u_j] = (I + sum_{l=j+1}^{k-1} E_l) B_j
     if (status == 0) {
-      const int k = lane;
+      const int k = S.lanef();
       double rmax[5 + NMPC_MAX_OBS];
       for (int i = 0; i < m; ++i) rmax[i] = 0.0;
       if (k <= N && k >= 1) {
@@ -1108,13 +1175,13 @@ __global__ __launch_bounds__(WAVE) void nmpc_solve_kernel(const Params* __restri
 
   // ---------------- initial point
   if (status == 0) {
-    for (int r = lane; r < ng; r += WAVE) {
+    for (int r = S.lanef(); r < ng; r += WAVE) {
       S.dl[r] = S.dc[r] * S.dl[r];
       S.du[r] = S.dc[r] * S.du[r];
     }
     int cx = 0, cs = 0;
     const double kp = o.bound_push, kf_ = o.bound_frac;
-    for (int i = lane; i < nw; i += WAVE) {
+    for (int i = S.lanef(); i < nw; i += WAVE) {
       const double lo = S.xl[i], hi = S.xu[i];
       const bool hl = S.hasl(lo), hu = S.hasu(hi);
       double x = S.U[i];
@@ -1131,7 +1198,7 @@ __global__ __launch_bounds__(WAVE) void nmpc_solve_kernel(const Params* __restri
     S.eval_fg(S.X, S.d, S.dc);
     S.derivs(S.X, S.U);
     const double skp = o.slack_bound_push, skf = o.slack_bound_frac;
-    for (int r = lane; r < ng; r += WAVE) {
+    for (int r = S.lanef(); r < ng; r += WAVE) {
       const double lo = S.dl[r], hi = S.du[r];
       const bool hl = S.hasl(lo), hu = S.hasu(hi);
       double x = S.d[r];
@@ -1149,13 +1216,13 @@ __global__ __launch_bounds__(WAVE) void nmpc_solve_kernel(const Params* __restri
     sync();
     // least-squares constraint multipliers: (I + J^T J) wx = bx + J^T bs ; y = bs - J wx
     if (o.constr_mult_init_max > 0 && ng > 0) {
-      for (int i = lane; i < nw; i += WAVE) { S.sigx[i] = 1.0; S.ru[i] = S.zl[i] - S.zu[i]; }
+      for (int i = S.lanef(); i < nw; i += WAVE) { S.sigx[i] = 1.0; S.ru[i] = S.zl[i] - S.zu[i]; }
       S.delta = 0.0;
-      S.summaries(SUM_LS);
-      S.riccati(0.0, -S.df, false, S.sigx, S.ru);
+      S.assemble(SUM_LS, 0.0, -S.df, false);
+      S.riccati(S.sigx, S.ru);
       S.forward(S.dU, S.dX);
       double ymax = 0.0;
-      for (int r = lane; r < ng; r += WAVE) {
+      for (int r = S.lanef(); r < ng; r += WAVE) {
         // y = bs - J wx with J wx = Gt dX
         const int k = r / m, i = r - k * m;
         const LDS double* xk = S.X + k * 8;
@@ -1175,14 +1242,14 @@ __global__ __launch_bounds__(WAVE) void nmpc_solve_kernel(const Params* __restri
       ymax = wmax(ymax);
       sync();
       if (!(ymax <= o.constr_mult_init_max)) {
-        for (int r = lane; r < ng; r += WAVE) S.y[r] = 0.0;
+        for (int r = S.lanef(); r < ng; r += WAVE) S.y[r] = 0.0;
       }
       sync();
     }
   }
 
 #ifdef NMPC_STAMPS
-  if (lane == 0) stamps[PH_INIT] += (double)(__builtin_amdgcn_s_memtime() - _tk0);
+  if (S.lanef() == 0) stamps[PH_INIT] += (double)(__builtin_amdgcn_s_memtime() - _tk0);
 #endif
   // ---------------- main loop
   double f = 0.0;
@@ -1206,7 +1273,7 @@ __global__ __launch_bounds__(WAVE) void nmpc_solve_kernel(const Params* __restri
     // ===== optimality error (IpoptCalculatedQuantities::curr_nlp_error)
     double dinf = 0, cviol = 0, ucviol = 0, cmp = 0, sumy = 0, sumz = 0, sumv = 0, pinf = 0;
     bool bad = false;
-    for (int i = lane; i < nw; i += WAVE) {
+    for (int i = S.lanef(); i < nw; i += WAVE) {
       const double g = S.grad_u(i) - S.zl[i] + S.zu[i];
       if (!isfinite(g)) bad = true;
       dinf = fmax(dinf, fabs(g));
@@ -1214,7 +1281,7 @@ __global__ __launch_bounds__(WAVE) void nmpc_solve_kernel(const Params* __restri
       if (S.hasu(S.xu[i])) cmp = fmax(cmp, fabs((S.xu[i] - S.U[i]) * S.zu[i]));
       sumz += fabs(S.zl[i]) + fabs(S.zu[i]);
     }
-    for (int r = lane; r < ng; r += WAVE) {
+    for (int r = S.lanef(); r < ng; r += WAVE) {
       const double g = -S.y[r] - S.vl[r] + S.vu[r];
       dinf = fmax(dinf, fabs(g));
       double cv = 0.0;
@@ -1286,7 +1353,7 @@ __global__ __launch_bounds__(WAVE) void nmpc_solve_kernel(const Params* __restri
     STAMP1(PH_CONV);
 
     // ===== search direction with inertia correction (PDPerturbationHandler)
-    for (int i = lane; i < nw; i += WAVE) {
+    for (int i = S.lanef(); i < nw; i += WAVE) {
       const bool hl = S.hasl(S.xl[i]), hu = S.hasu(S.xu[i]);
       const double Sl = hl ? S.U[i] - S.xl[i] : 1.0, Su = hu ? S.xu[i] - S.U[i] : 1.0;
       S.sigx[i] = (hl ? S.zl[i] / Sl : 0.0) + (hu ? S.zu[i] / Su : 0.0);
@@ -1299,8 +1366,8 @@ __global__ __launch_bounds__(WAVE) void nmpc_solve_kernel(const Params* __restri
     bool fact_ok = false;
     while (true) {
       S.delta = delta;
-      S.summaries(SUM_NEWTON);
-      if (S.riccati(S.df, S.df, true, S.sigx, S.ru)) { fact_ok = true; break; }
+      S.assemble(SUM_NEWTON, S.df, S.df, true);
+      if (S.riccati(S.sigx, S.ru)) { fact_ok = true; break; }
       sync();
       if (delta == 0.0) {
         delta = (delta_last == 0.0) ? o.first_hessian_perturbation
@@ -1321,18 +1388,18 @@ __global__ __launch_bounds__(WAVE) void nmpc_solve_kernel(const Params* __restri
     double theta_ref = 0.0, gbd = 0.0;
     {
       double th = 0.0, g = 0.0;
-      for (int r = lane; r < ng; r += WAVE) {
+      for (int r = S.lanef(); r < ng; r += WAVE) {
         th += fabs(S.d[r] - S.s[r]);
         const bool hl = S.hasl(S.dl[r]), hu = S.hasu(S.du[r]);
         const double gs = -(hl ? mu / (S.s[r] - S.dl[r]) : 0.0) + (hu ? mu / (S.du[r] - S.s[r]) : 0.0) +
                           o.kappa_d * mu * ((hl && !hu ? 1.0 : 0.0) - (hu && !hl ? 1.0 : 0.0));
         g += gs * S.ds[r];
       }
-      for (int i = lane; i < nw; i += WAVE) g += S.ru[i] * S.dU[i];
-      if (lane <= N) {
+      for (int i = S.lanef(); i < nw; i += WAVE) g += S.ru[i] * S.dU[i];
+      if (S.lanef() <= N) {
         double gx = 0.0;
 #pragma unroll
-        for (int c = 0; c < 8; ++c) gx += S.gl[lane * 8 + c] * S.dX[lane * 8 + c];
+        for (int c = 0; c < 8; ++c) gx += S.gl[S.lanef() * 8 + c] * S.dX[S.lanef() * 8 + c];
         g += S.df * gx;
       }
       theta_ref = wsum(th);
@@ -1381,12 +1448,12 @@ __global__ __launch_bounds__(WAVE) void nmpc_solve_kernel(const Params* __restri
       const double a = fmin(ap, ad);
       // current pd error (grad_lag from the adjoint computed at loop start)
       double dual = 0, prim = 0, cm = 0;
-      for (int i = lane; i < nw; i += WAVE) {
+      for (int i = S.lanef(); i < nw; i += WAVE) {
         dual += fabs(S.grad_u(i) - S.zl[i] + S.zu[i]);
         if (S.hasl(S.xl[i])) cm += fabs((S.U[i] - S.xl[i]) * S.zl[i] - mu);
         if (S.hasu(S.xu[i])) cm += fabs((S.xu[i] - S.U[i]) * S.zu[i] - mu);
       }
-      for (int r = lane; r < ng; r += WAVE) {
+      for (int r = S.lanef(); r < ng; r += WAVE) {
         dual += fabs(-S.y[r] - S.vl[r] + S.vu[r]);
         prim += fabs(S.d[r] - S.s[r]);
         if (S.hasl(S.dl[r])) cm += fabs((S.s[r] - S.dl[r]) * S.vl[r] - mu);
@@ -1400,7 +1467,7 @@ __global__ __launch_bounds__(WAVE) void nmpc_solve_kernel(const Params* __restri
       // trial multipliers into the "2" buffers: dU2 <- (unused) ; stage them in place later
       // evaluate grad_lag at the trial point: derivatives + adjoint with trial y
       // (overwrites the current derivative data; if rejected the solve stops)
-      for (int r = lane; r < ng; r += WAVE) {
+      for (int r = S.lanef(); r < ng; r += WAVE) {
         double D, rs;
         S.row_rs(r, D, rs);
         S.dms[r] = S.y[r] + a * (D * S.ds[r] + rs);  // trial y
@@ -1412,7 +1479,7 @@ __global__ __launch_bounds__(WAVE) void nmpc_solve_kernel(const Params* __restri
       S.adjoint(S.df, S.dms);
       S.X = Xs;
       double dual2 = 0, prim2 = 0, cm2 = 0;
-      for (int i = lane; i < nw; i += WAVE) {
+      for (int i = S.lanef(); i < nw; i += WAVE) {
         double dzl, dzu;
         S.dz_x(i, S.dU[i], dzl, dzu);
         const double zlt = S.zl[i] + a * dzl, zut = S.zu[i] + a * dzu;
@@ -1420,7 +1487,7 @@ __global__ __launch_bounds__(WAVE) void nmpc_solve_kernel(const Params* __restri
         if (S.hasl(S.xl[i])) cm2 += fabs((S.Ut[i] - S.xl[i]) * zlt - mu);
         if (S.hasu(S.xu[i])) cm2 += fabs((S.xu[i] - S.Ut[i]) * zut - mu);
       }
-      for (int r = lane; r < ng; r += WAVE) {
+      for (int r = S.lanef(); r < ng; r += WAVE) {
         double dvl, dvu;
         S.dv_s(r, S.ds[r], dvl, dvu);
         const double vlt = S.vl[r] + a * dvl, vut = S.vu[r] + a * dvu;
@@ -1450,8 +1517,8 @@ __global__ __launch_bounds__(WAVE) void nmpc_solve_kernel(const Params* __restri
     } else {
       // tiny step detection (BacktrackingLineSearch::DetectTinyStep)
       double mx = 0.0, msv = 0.0;
-      for (int i = lane; i < nw; i += WAVE) mx = fmax(mx, fabs(S.dU[i] / (1.0 + fabs(S.U[i]))));
-      for (int r = lane; r < ng; r += WAVE) msv = fmax(msv, fabs(S.ds[r] / (1.0 + fabs(S.s[r]))));
+      for (int i = S.lanef(); i < nw; i += WAVE) mx = fmax(mx, fabs(S.dU[i] / (1.0 + fabs(S.U[i]))));
+      for (int r = S.lanef(); r < ng; r += WAVE) msv = fmax(msv, fabs(S.ds[r] / (1.0 + fabs(S.s[r]))));
       mx = wmax(mx); msv = wmax(msv);
       const bool tiny = mx <= o.tiny_step_tol && msv <= o.tiny_step_tol && pinf <= 1e-4;
       if (tiny) {
@@ -1484,21 +1551,21 @@ __global__ __launch_bounds__(WAVE) void nmpc_solve_kernel(const Params* __restri
           if (okev && a == amax_p && theta_ref <= tht && o.max_soc > 0) {
             // second-order correction (FilterLSAcceptor::TrySecondOrderCorrection)
             double th_tr = tht, th_old = 0.0, a_soc = a;
-            for (int r = lane; r < ng; r += WAVE) S.dms[r] = S.d[r] - S.s[r];
+            for (int r = S.lanef(); r < ng; r += WAVE) S.dms[r] = S.d[r] - S.s[r];
             int cnt = 0;
             bool soc_acc = false;
-            const LDS double* dsp = S.ds;  // step whose trial is in Ut/dt
+            const GLB double* dsp = S.ds;  // step whose trial is in Ut/dt
             while (cnt < o.max_soc && (cnt == 0 || th_tr <= o.kappa_soc * th_old)) {
               th_old = th_tr;
-              for (int r = lane; r < ng; r += WAVE) {
+              for (int r = S.lanef(); r < ng; r += WAVE) {
                 const double sv = S.s[r] + a_soc * dsp[r];
                 S.dms[r] = a_soc * S.dms[r] + (S.dt[r] - sv);
               }
               sync();
-              S.summaries(SUM_SOC);
-              S.resolve(S.df, S.ru);
-              S.forward(S.dU2, S.dX2);
-              S.row_step(S.dX2, S.dms, true, S.ds2);
+              S.assemble(SUM_SOC, S.df, S.df, true);
+              S.resolve(S.ru);
+              S.forward(S.dU2, S.dX);   // dX is free once gBD is known
+              S.row_step(S.dX, S.dms, true, S.ds2);
               a_soc = S.frac_to_bound(tau, S.dU2, S.ds2);
               dsp = S.ds2;
               double ft2, phit2, tht2;
@@ -1532,13 +1599,13 @@ __global__ __launch_bounds__(WAVE) void nmpc_solve_kernel(const Params* __restri
     // ===== accept the trial point (IpoptAlgorithm::AcceptTrialPoint)
     {
       STAMP0();
-      const LDS double* dUa = (acc_kind == 2) ? S.dU2 : S.dU;
-      const LDS double* dsa = (acc_kind == 2) ? S.ds2 : S.ds;
+      const GLB double* dUa = (acc_kind == 2) ? S.dU2 : S.dU;
+      const GLB double* dsa = (acc_kind == 2) ? S.ds2 : S.ds;
       if (acc_kind != 3) alpha_d = S.dual_frac_to_bound(tau, dUa, dsa);
       const double ap = alpha_p, ad = alpha_d;
       const double ks = o.kappa_sigma;
       // bound multipliers of U (old slacks for the step, new slacks for kappa_sigma)
-      for (int i = lane; i < nw; i += WAVE) {
+      for (int i = S.lanef(); i < nw; i += WAVE) {
         double dzl, dzu;
         S.dz_x(i, dUa[i], dzl, dzu);
         double nzl = S.zl[i] + ad * dzl, nzu = S.zu[i] + ad * dzu;
@@ -1549,7 +1616,7 @@ __global__ __launch_bounds__(WAVE) void nmpc_solve_kernel(const Params* __restri
         else nzu = 0.0;
         S.zl[i] = nzl; S.zu[i] = nzu;
       }
-      for (int r = lane; r < ng; r += WAVE) {
+      for (int r = S.lanef(); r < ng; r += WAVE) {
         double D, rs, dvl, dvu;
         S.row_rs(r, D, rs);
         S.dv_s(r, dsa[r], dvl, dvu);
@@ -1565,10 +1632,10 @@ __global__ __launch_bounds__(WAVE) void nmpc_solve_kernel(const Params* __restri
         S.s[r] = sn;
         S.d[r] = S.dt[r];
       }
-      for (int i = lane; i < nw; i += WAVE) S.U[i] = S.Ut[i];
-      if (lane <= N) {
+      for (int i = S.lanef(); i < nw; i += WAVE) S.U[i] = S.Ut[i];
+      if (S.lanef() <= N) {
 #pragma unroll
-        for (int c = 0; c < 8; ++c) S.X[lane * 8 + c] = S.Xt[lane * 8 + c];
+        for (int c = 0; c < 8; ++c) S.X[S.lanef() * 8 + c] = S.Xt[S.lanef() * 8 + c];
       }
       sync();
       f = f_acc;
@@ -1580,7 +1647,7 @@ __global__ __launch_bounds__(WAVE) void nmpc_solve_kernel(const Params* __restri
       }
     }
     ++it;
-    if (trace && lane == 0) {
+    if (trace && S.lanef() == 0) {
       double th = 0.0;
       for (int r = 0; r < ng; ++r) th += fabs(S.d[r] - S.s[r]);
       double* t = trace + (long long)(it - 1) * TRACE_F;
@@ -1591,34 +1658,34 @@ __global__ __launch_bounds__(WAVE) void nmpc_solve_kernel(const Params* __restri
   }
 
   // ---------------- outputs (honor_original_bounds)
-  for (int i = lane; i < nw; i += WAVE) {
+  for (int i = S.lanef(); i < nw; i += WAVE) {
     const double lo = io.lbx[(long long)b * io.ld_lbx + i], hi = io.ubx[(long long)b * io.ld_ubx + i];
     S.Ut[i] = fmin(fmax(S.U[i], lo), hi);
   }
   sync();
   S.rollout(S.Ut, S.Xt);
   const double fo = S.eval_fg(S.Xt, S.dt, nullptr);
-  for (int i = lane; i < nw; i += WAVE) {
+  for (int i = S.lanef(); i < nw; i += WAVE) {
     io.x_out[(long long)b * nw + i] = S.Ut[i];
     if (io.lam_x) io.lam_x[(long long)b * nw + i] = (S.zu[i] - S.zl[i]) / S.df;
   }
-  for (int r = lane; r < ng; r += WAVE) {
+  for (int r = S.lanef(); r < ng; r += WAVE) {
     if (io.g_out) io.g_out[(long long)b * ng + r] = S.dt[r];
     if (io.lam_g) io.lam_g[(long long)b * ng + r] = S.y[r] * S.dc[r] / S.df;
   }
   if (io.X_out) {
     const int nX = prm->nX;
-    for (int i = lane; i < nX; i += WAVE) io.X_out[(long long)b * nX + i] = S.Xt[i];
+    for (int i = S.lanef(); i < nX; i += WAVE) io.X_out[(long long)b * nX + i] = S.Xt[i];
   }
 #ifdef NMPC_STAMPS
   if (trace) {
     sync();
-    if (lane == 0) stamps[PH_TOTAL] = (double)(__builtin_amdgcn_s_memtime() - _tk0);
+    if (S.lanef() == 0) stamps[PH_TOTAL] = (double)(__builtin_amdgcn_s_memtime() - _tk0);
     sync();
-    if (lane < PH_COUNT) trace[(long long)max_iter * TRACE_F + lane] = stamps[lane];
+    if (S.lanef() < PH_COUNT) trace[(long long)max_iter * TRACE_F + S.lanef()] = stamps[S.lanef()];
   }
 #endif
-  if (lane == 0) {
+  if (S.lanef() == 0) {
     if (io.f_out) io.f_out[b] = fo;
     if (io.status) io.status[b] = status;
     if (io.iters) io.iters[b] = it;
@@ -1659,6 +1726,8 @@ int fail(int code, const std::string& msg) {
 
 }  // namespace
 
+typedef void (*KernFn)(const Params*, int, IO);
+
 struct nmpc_handle {
   Params hp;
   Params* dprm = nullptr;
@@ -1669,27 +1738,28 @@ struct nmpc_handle {
   size_t dbuf_bytes = 0;
   int* ibuf = nullptr;
   size_t ibuf_bytes = 0;
+  KernFn kern = nullptr;
+  int ws_doubles = 0;
   bool trace = false;
   double* dtrace = nullptr;
+  double* dws = nullptr;       // per-scenario global workspace
+  size_t ws_bytes = 0;
   size_t trace_bytes = 0;
   int last_B = 0;
 };
 
-static int layout(Params& P) {
-  int off = 0;
-  auto al = [&](int n) { int o = off; off += (n + 1) & ~1; return o; };
-  const int nw = P.nw, ng = P.ng, nX = P.nX, NS = P.N + 1;
-  P.U = al(nw); P.Ut = al(nw); P.dU = al(nw); P.dU2 = al(nw); P.zl = al(nw); P.zu = al(nw);
-  P.xl = al(nw); P.xu = al(nw); P.sigx = al(nw); P.ru = al(nw);
-  P.X = al(nX); P.Xt = al(nX); P.dX = al(nX); P.dX2 = al(nX);
-  P.s = al(ng); P.y = al(ng); P.vl = al(ng); P.vu = al(ng); P.d = al(ng); P.dt = al(ng);
-  P.ds = al(ng); P.ds2 = al(ng); P.dc = al(ng); P.dl = al(ng); P.du = al(ng); P.dms = al(ng);
-  P.gl = al(8 * NS); P.Hl = al(21 * NS); P.trig = al(8 * NS); P.st = al(16 * NS); P.lam = al(8 * NS);
-  P.K = al(48 * P.N); P.kf = al(6 * P.N); P.Lc = al(28 * P.N);
-  P.P0 = al(64); P.P1 = al(64); P.pv0 = al(8); P.pv1 = al(8); P.PA = al(64); P.BtP = al(48); P.St = al(48); P.Rt = al(22);
-  P.p = al(64); P.ob = al(2 * NMPC_MAX_OBS); P.inc = al(8 * 64); P.filt = al(2 * FCAP + 2); P.red = al(64);
-  P.total = off;
-  return off * 8;
+using CapA = Cap<20, 15>;   // BASELINE configs 2-4 (N=20, <=10 obstacles) and the reference's N=15 scripts
+using CapB = Cap<31, 21>;
+using CapC = Cap<63, 21>;   // any supported shape
+
+static void pick_class(const Params& P, KernFn* fn, int* lds_doubles, int* ws_doubles) {
+  if (P.N <= CapA::nmax && P.m <= CapA::mmax) {
+    *fn = nmpc_solve_kernel<CapA>; *lds_doubles = CapA::L.total; *ws_doubles = CapA::L.wstotal;
+  } else if (P.N <= CapB::nmax && P.m <= CapB::mmax) {
+    *fn = nmpc_solve_kernel<CapB>; *lds_doubles = CapB::L.total; *ws_doubles = CapB::L.wstotal;
+  } else {
+    *fn = nmpc_solve_kernel<CapC>; *lds_doubles = CapC::L.total; *ws_doubles = CapC::L.wstotal;
+  }
 }
 
 extern "C" {
@@ -1742,7 +1812,11 @@ int nmpc_create(const nmpc_desc* desc, nmpc_handle** out) {
     P.oxp[j] = desc->obs_x_pidx[j]; P.oyp[j] = desc->obs_y_pidx[j];
   }
   P.o = desc->opts;
-  h->lds_bytes = layout(P);
+  {
+    int ldsd = 0;
+    pick_class(P, &h->kern, &ldsd, &h->ws_doubles);
+    h->lds_bytes = ldsd * 8;
+  }
   if (h->lds_bytes > 160 * 1024) {
     delete h;
     return fail(NMPC_E_INVALID, "problem too large for the LDS-resident kernel (N*(5+n_obs) too big)");
@@ -1752,7 +1826,7 @@ int nmpc_create(const nmpc_desc* desc, nmpc_handle** out) {
   if (hipMemcpy(h->dprm, &P, sizeof(Params), hipMemcpyHostToDevice) != hipSuccess) {
     hipFree(h->dprm); delete h; return fail(NMPC_E_HIP, "hipMemcpy params");
   }
-  if (hipFuncSetAttribute((const void*)nmpc_solve_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+  if (hipFuncSetAttribute((const void*)h->kern, hipFuncAttributeMaxDynamicSharedMemorySize,
                           h->lds_bytes) != hipSuccess) {
     hipFree(h->dprm); delete h; return fail(NMPC_E_HIP, "hipFuncSetAttribute(MaxDynamicSharedMemorySize)");
   }
@@ -1766,6 +1840,7 @@ int nmpc_destroy(nmpc_handle* h) {
   if (h->dbuf) hipFree(h->dbuf);
   if (h->ibuf) hipFree(h->ibuf);
   if (h->dtrace) hipFree(h->dtrace);
+  if (h->dws) hipFree(h->dws);
   delete h;
   return NMPC_OK;
 }
@@ -1831,8 +1906,18 @@ int nmpc_solve_batch_dev(nmpc_handle* h, int32_t B, const double* x0, int64_t ld
     hipMemsetAsync(h->dtrace, 0, need, (hipStream_t)stream);
     io.trace = h->dtrace;
   }
+  {
+    const size_t need = (size_t)B * h->ws_doubles * sizeof(double);
+    if (need > h->ws_bytes) {
+      if (h->dws) hipFree(h->dws);
+      h->dws = nullptr; h->ws_bytes = 0;
+      if (hipMalloc(&h->dws, need) != hipSuccess) return fail(NMPC_E_NOMEM, "hipMalloc workspace");
+      h->ws_bytes = need;
+    }
+    io.ws = h->dws;
+  }
   h->last_B = B;
-  hipLaunchKernelGGL(nmpc_solve_kernel, dim3(B), dim3(WAVE), h->lds_bytes, (hipStream_t)stream,
+  hipLaunchKernelGGL(h->kern, dim3(B), dim3(WAVE), h->lds_bytes, (hipStream_t)stream,
                      (const Params*)h->dprm, (int)B, io);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return fail(NMPC_E_HIP, std::string("kernel launch: ") + hipGetErrorString(e));
