@@ -1,10 +1,16 @@
 """Benchmark: batched NMPC steps/s on MI355X (BASELINE.json metric).
 
-One *step* = one batched MPC step over B scenarios per GPU: every scenario's
-per-timestep NLP (Python/NMPC_TT.py:358-365) solved by the HIP kernel,
-warm-started from the previous step's shifted solution, followed by the
-closed-loop shift on device (Python/NMPC_TT.py:13-30) and, for N>1 GPUs, the
-RCCL gather of each scenario's applied control and status to rank 0.
+One *MPC step* = one scenario's per-timestep NLP (Python/NMPC_TT.py:358-365)
+solved to termination, warm-started from the previous step's shifted solution,
+followed by the closed-loop shift (Python/NMPC_TT.py:13-30).  A bench *step*
+advances all B scenarios per GPU by one MPC step; --steps K of them are timed
+(K=20 warm-started closed-loop steps per scenario is the headline).
+
+Default mode "fused": the K steps run in ONE launch (nmpc_closed_loop_dev), each
+scenario's closed loop on its own wavefront, so a step never waits for another
+scenario's slowest solve; for N>1 GPUs the per-step results are RCCL-gathered
+once at the end.  The one-launch-per-step mode (solve launch + shift launch,
+gather every step) is timed from the same state and reported beside it.
 
 Workload (config 3 of BASELINE.json / SURVEY.md section 8): 4096 scenarios
 per GPU, N=20, 10 static obstacles (Python/Race Track 2.py layout), T=0.2,
@@ -41,8 +47,8 @@ def survey_bytes_per_step(spec, ibar):
     return ibar * b_iter + io, s_stage, b_iter, io
 
 
-def pmc_traffic():
-    """HBM bytes per solve launch from the newest committed rocprofv3 PMC pass
+def pmc_traffic(kernel="nmpc_closed_loop_kernel"):
+    """HBM bytes per launch of `kernel` from the newest committed rocprofv3 PMC pass
     (profiles/r*_pmc_fetch_write.csv): FETCH_SIZE is doubled per the gfx950
     correction (MI355X_MICROARCH.md, HBM section), WRITE_SIZE taken as is; KB -> B."""
     import csv
@@ -52,7 +58,7 @@ def pmc_traffic():
         return None, None
     fetch, write = [], []
     for row in csv.DictReader(open(files[-1])):
-        if "nmpc_solve_kernel" not in row.get("Kernel_Name", ""):
+        if kernel not in row.get("Kernel_Name", ""):
             continue
         (fetch if row["Counter_Name"] == "FETCH_SIZE" else write).append(float(row["Counter_Value"]))
     if not fetch or not write:
@@ -86,12 +92,15 @@ def cpu_baseline(spec_cfg, P, lbx, ubx, lbg, ubg, budget_s=15.0):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--steps", type=int, default=20, help="closed-loop MPC steps per scenario (timed)")
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--batch", type=int, default=4096, help="scenarios per GPU")
     ap.add_argument("--config", type=int, default=3)
-    ap.add_argument("--mode", choices=["closed_loop", "cold"], default="closed_loop")
+    ap.add_argument("--mode", choices=["fused", "per_step", "cold"], default="fused",
+                    help="fused: K closed-loop steps per scenario in one launch (nmpc_closed_loop_dev); "
+                         "per_step: one solve launch + shift launch per step; cold: per step, u=0 each step")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-per-step", action="store_true", help="skip the per-step-launch comparison line")
     ap.add_argument("--cpu-budget", type=float, default=15.0)
     args = ap.parse_args()
 
@@ -109,7 +118,7 @@ def main():
     dev = torch.device("cuda", local_rank if world > 1 else 0)
 
     spec = config_spec(args.config)
-    B = args.batch
+    B, K, W = args.batch, args.steps, args.warmup
     # global scenario stream, sliced per rank (results independent of world size)
     P_all = draw_scenarios(spec, B * world, seed=1000 + args.config)
     P = P_all[shard(B * world, world, rank)]
@@ -117,96 +126,131 @@ def main():
     solver = nlpsol("solver", "ipopt", spec, REFERENCE_OPTS)
 
     f64 = dict(dtype=torch.float64, device=dev)
-    t_lbx, t_ubx = torch.tensor(lbx, **f64), torch.tensor(ubx, **f64)
-    t_lbg, t_ubg = torch.tensor(lbg, **f64), torch.tensor(ubg, **f64)
-    p = torch.tensor(P, **f64).contiguous()
-    w = torch.zeros(B, spec.nw, **f64)
-    out = {"x": torch.empty(B, spec.nw, **f64), "f": torch.empty(B, **f64),
-           "status": torch.empty(B, dtype=torch.int32, device=dev),
-           "iters": torch.empty(B, dtype=torch.int32, device=dev)}
+    i32 = dict(dtype=torch.int32, device=dev)
+    bnd = [torch.tensor(v, **f64) for v in (lbx, ubx, lbg, ubg)]
+    p0 = torch.tensor(P, **f64).contiguous()
+    w0 = torch.zeros(B, spec.nw, **f64)
     v_t = torch.full((B,), 12.0, **f64)   # target speed, Python/NMPC_TT.py:25
     w_t = torch.full((B,), 0.01, **f64)   # target turn rate
     stream = torch.cuda.current_stream()
 
-    status_hist = {}
+    def hist_bufs(k):
+        return {"u": torch.empty(k, B, 6, **f64), "f": torch.empty(k, B, **f64),
+                "status": torch.empty(k, B, **i32), "iters": torch.empty(k, B, **i32)}
 
-    iters_hist = torch.zeros(max(args.steps, args.warmup), B, dtype=torch.int32, device=dev)
-    st_hist = torch.zeros(max(args.steps, args.warmup), B, dtype=torch.int32, device=dev)
+    out = {"x": torch.empty(B, spec.nw, **f64), "f": torch.empty(B, **f64),
+           "status": torch.empty(B, **i32), "iters": torch.empty(B, **i32)}
 
-    def one_step(k, timed_events=None):
-        # identical work in warmup and timed steps (torch kernels load lazily on first use)
+    def per_step(p, w, hist, k, cold, timed_events=None):
+        """One batched step: solve launch (+ shift launch) (+ per-step gather)."""
         if timed_events is not None:
             timed_events[0].record(stream)
-        solver.solve_device(w if args.mode == "closed_loop" else torch.zeros_like(w),
-                            t_lbx, t_ubx, t_lbg, t_ubg, p, out, stream=stream)
+        solver.solve_device(torch.zeros_like(w) if cold else w, *bnd, p, out, stream=stream)
         if timed_events is not None:
             timed_events[1].record(stream)
-        if args.mode == "closed_loop":
+        if not cold:
             solver.shift_device(p, out["x"], w, v_t, w_t, stream=stream)
-        if world > 1:  # the only exchange: per-step gather of (u0, f, status) to every rank
+        if world > 1:  # per-step gather of (u0, f, status)
             gather_rows(pack_result(out["x"], out["f"], out["status"]), world)
-        iters_hist[k].copy_(out["iters"])
-        st_hist[k].copy_(out["status"])
+        hist["u"][k].copy_(out["x"][:, :6]); hist["f"][k].copy_(out["f"])
+        hist["iters"][k].copy_(out["iters"]); hist["status"][k].copy_(out["status"])
 
-    for k in range(args.warmup):
-        one_step(k)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
-    t0 = time.perf_counter()
-    for k in range(args.steps):
-        one_step(k, evs[k])
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    kern_ms = [a.elapsed_time(b) for a, b in evs]
-    el_t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-    iters_sum = iters_hist[:args.steps].sum()
-    tot = torch.stack([iters_sum.double(), torch.tensor(float(B * args.steps), **f64)])
-    if world > 1:
-        dist.all_reduce(el_t, op=dist.ReduceOp.MAX)
-        dist.all_reduce(tot, op=dist.ReduceOp.SUM)
-    elapsed = float(el_t.item())
-    ibar = float(tot[0].item() / tot[1].item())
-    sts = st_hist[:args.steps].cpu().numpy()
-    for s_ in np.unique(sts):
-        status_hist[int(s_)] = int((sts == s_).sum())
+    def fused(p, w, hist, k_steps, timed_events=None):
+        if timed_events is not None:
+            timed_events[0].record(stream)
+        solver.closed_loop_device(k_steps, *bnd, p, w, v_t, w_t, hist, stream=stream)
+        if timed_events is not None:
+            timed_events[1].record(stream)
+        if world > 1:  # the only exchange: final gather of every step's (u0, f, status)
+            gather_rows(torch.cat([hist["u"].permute(1, 0, 2).reshape(B, -1), hist["f"].t(),
+                                   hist["status"].t().double()], dim=1).contiguous(), world)
+
+    def barrier_sync():
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    def timed_run(mode, p, w):
+        """Warmup W steps (advancing the closed loop), then time exactly K steps."""
+        hw, ht = hist_bufs(max(W, 1)), hist_bufs(K)
+        if mode == "fused":
+            if W:
+                fused(p, w, hw, W)
+            # the same launch shape once more on scratch copies (code objects, workspace)
+            fused(p.clone(), w.clone(), hist_bufs(K), K)
+        else:
+            for k in range(W):
+                per_step(p, w, hw, k, mode == "cold")
+        barrier_sync()
+        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+               for _ in range(1 if mode == "fused" else K)]
+        t0 = time.perf_counter()
+        if mode == "fused":
+            fused(p, w, ht, K, evs[0])
+        else:
+            for k in range(K):
+                per_step(p, w, ht, k, mode == "cold", evs[k])
+        barrier_sync()
+        elapsed = time.perf_counter() - t0
+        kern_ms = [a.elapsed_time(b) for a, b in evs]
+        el_t = torch.tensor([elapsed], **f64)
+        tot = torch.stack([ht["iters"].sum().double(), torch.tensor(float(B * K), **f64)])
+        if world > 1:
+            dist.all_reduce(el_t, op=dist.ReduceOp.MAX)
+            dist.all_reduce(tot, op=dist.ReduceOp.SUM)
+        sts = ht["status"].cpu().numpy()
+        hist = {int(s_): int((sts == s_).sum()) for s_ in np.unique(sts)}
+        return float(el_t.item()), kern_ms, float(tot[0].item() / tot[1].item()), hist
+
+    elapsed, kern_ms, ibar, status_hist = timed_run(args.mode, p0.clone(), w0.clone())
+    side = None
+    if args.mode == "fused" and not args.no_per_step:
+        e2, km2, ib2, h2 = timed_run("per_step", p0.clone(), w0.clone())
+        side = {"mode": "per_step (one solve launch + one shift launch per MPC step)",
+                "value": B * world * K / e2, "ms_per_step": e2 / K * 1e3,
+                "kernel_avg_ms": float(np.mean(km2)), "kernel_max_ms": float(np.max(km2)),
+                "mean_ip_iterations": ib2, "status_histogram": h2}
 
     if rank == 0:
-        total_steps = B * world * args.steps
+        total_steps = B * world * K
         value = total_steps / elapsed
-        ms_per_step = elapsed / args.steps * 1e3
+        ms_per_step = elapsed / K * 1e3
+        n_launch = len(kern_ms)
         kern_avg_s = float(np.mean(kern_ms)) / 1e3
-        flops_launch = B * ibar * (spec.N + 1) * KFLOP_PER_STAGE_ITER * 1e3
+        steps_per_launch = K if args.mode == "fused" else 1
+        kname = "nmpc_closed_loop_kernel" if args.mode == "fused" else "nmpc_solve_kernel"
+        flops_launch = B * steps_per_launch * ibar * (spec.N + 1) * KFLOP_PER_STAGE_ITER * 1e3
         achieved = flops_launch / kern_avg_s / 1e12
         bps, s_stage, b_iter, io = survey_bytes_per_step(spec, ibar)
-        traffic, traffic_src = pmc_traffic()
+        traffic, traffic_src = pmc_traffic(kname)
+        mode_txt = {"fused": f"{K} warm-started closed-loop MPC steps per scenario in one launch",
+                    "per_step": "warm-started closed-loop MPC steps, one launch per step",
+                    "cold": "cold-start (u=0) solves, one launch per step"}[args.mode]
         res = {
             "metric": "MPC steps/sec (batched scenarios), N=20 UAV+gimbal, 10 obstacles",
-            "value": value, "unit": "MPC steps/s", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": True,
+            "value": value, "unit": "MPC steps/s", "n_gpus": world, "steps": K,
+            "warmup": W, "ms_per_step": ms_per_step, "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
             "config": {"workload": f"config {args.config}: batch={B}/GPU, N={spec.N}, {spec.n_obs} static "
-                                   f"obstacles (Race Track 2.py), T={spec.T}, reference IPOPT opts, "
-                                   f"{args.mode.replace('_', '-')} warm-started MPC steps",
+                                   f"obstacles (Race Track 2.py), T={spec.T}, reference IPOPT opts, {mode_txt}",
                        "global_batch": B * world, "seq_len": spec.N, "parallelism": f"dp{world}"},
             "roofline": {"bound": "mfma", "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                          "frac": achieved / FP64_PEAK_TFLOPS, "traffic": traffic,
                          "traffic_unit": "HBM bytes per launch (2*FETCH_SIZE + WRITE_SIZE)",
                          "traffic_source": traffic_src,
-                         "kernel": "nmpc_solve_kernel", "kernel_avg_ms": kern_avg_s * 1e3,
+                         "kernel": kname, "kernel_avg_ms": kern_avg_s * 1e3, "launches": n_launch,
                          "model": f"SURVEY 8(d) {KFLOP_PER_STAGE_ITER} kflop/stage-iteration x (N+1) x "
-                                  f"I_bar={ibar:.2f} x B per launch; FP64 peak (vector = matrix)"},
+                                  f"I_bar={ibar:.2f} x B x {steps_per_launch} step(s) per launch; "
+                                  f"FP64 peak (vector = matrix)"},
             "survey_hbm_model": {"bytes_per_step": bps, "S_stage": s_stage, "B_iter": b_iter, "IO": io,
-                                 "equivalent_GBs": B * bps / kern_avg_s / 1e9,
-                                 "io_only_GBs": B * io / kern_avg_s / 1e9},
+                                 "equivalent_GBs": B * steps_per_launch * bps / kern_avg_s / 1e9,
+                                 "io_only_GBs": B * steps_per_launch * io / kern_avg_s / 1e9},
             "mean_ip_iterations": ibar,
             "status_histogram": status_hist,
         }
+        if side is not None:
+            res["per_step_launch"] = side
         if world == 1 and not args.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline(spec, P, lbx, ubx, lbg, ubg, budget_s=args.cpu_budget)
         print(json.dumps(res))

@@ -1054,14 +1054,9 @@ struct Solver {
 };
 
 // ------------------------------------------------------------------ kernel
+// One scenario's solve (the whole IPOPT loop) by the calling wavefront.
 template <class CAP>
-__global__ __launch_bounds__(WAVE, 2) void nmpc_solve_kernel(const Params* __restrict__ prm, int B, IO io) {
-  extern __shared__ __attribute__((aligned(16))) double smem[];
-  const int b = blockIdx.x;
-  if (b >= B) return;
-  const int lane = threadIdx.x;
-  Solver<CAP> S;
-  S.bind(prm, smem, io.ws, lane, b);
+__device__ __forceinline__ void solve_one(Solver<CAP>& S, const Params* __restrict__ prm, const IO& io, const int b) {
   auto lanef = [&]() { return S.lanef(); };  // for the STAMP macros
   (void)lanef;
   LDS double* stamps = S.stamps;
@@ -1692,6 +1687,91 @@ __global__ __launch_bounds__(WAVE, 2) void nmpc_solve_kernel(const Params* __res
   }
 }
 
+template <class CAP>
+__global__ __launch_bounds__(WAVE, 2) void nmpc_solve_kernel(const Params* __restrict__ prm, int B, IO io) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  const int b = blockIdx.x;
+  if (b >= B) return;
+  Solver<CAP> S;
+  S.bind(prm, smem, io.ws, threadIdx.x, b);
+  solve_one<CAP>(S, prm, io, b);
+}
+
+// K-step closed loop per scenario in ONE launch (Python/NMPC_TT.py:348-402 main loop):
+// solve, record (x0, u0, f, status, iters), then shift_timestep (:13-30) -- each wave
+// advances its own scenario, so no step waits for another scenario's slowest solve.
+struct Loop {
+  int K;
+  double* p;          // np x B (ld_p), advanced in place
+  long long ld_p;
+  double* w;          // nw x B warm start, in/out (holds the shifted last solution on exit)
+  const double *vt, *wt;
+  double *u_hist, *x_hist, *f_hist;  // K x B x 6, K x B x 8, K x B (nullable)
+  int *st_hist, *it_hist;            // K x B (nullable)
+};
+
+template <class CAP>
+__global__ __launch_bounds__(WAVE, 2) void nmpc_closed_loop_kernel(const Params* __restrict__ prm, int B, IO io,
+                                                                    Loop lp) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  const int b = blockIdx.x;
+  if (b >= B) return;
+  Solver<CAP> S;
+  S.bind(prm, smem, io.ws, threadIdx.x, b);
+  const int nw = S.nw, N = S.N;
+  const double T = S.T;
+  double* wb = lp.w + (long long)b * nw;
+  double* pb = lp.p + (long long)b * lp.ld_p;
+  constexpr int WR = (6 * CAP::nmax + WAVE - 1) / WAVE;
+  for (int k = 0; k < lp.K; ++k) {
+    // re-derive every per-lane address each step from an opaque lane index, so the
+    // compiler keeps nothing live across steps (hoisting them costs ~40 VGPRs of spills)
+    S.bind(prm, smem, io.ws, S.lanef(), b);
+    IO ik = io;
+    ik.x0 = lp.w; ik.ld_x0 = nw; ik.x_out = lp.w;
+    ik.p = lp.p; ik.ld_p = lp.ld_p;
+    const long long kb = (long long)k * B;
+    ik.f_out = lp.f_hist ? lp.f_hist + kb : nullptr;
+    ik.status = lp.st_hist ? lp.st_hist + kb : nullptr;
+    ik.iters = lp.it_hist ? lp.it_hist + kb : nullptr;
+    solve_one<CAP>(S, prm, ik, b);
+    sync();
+    // shift_timestep: read the solution and the state before anything is overwritten
+    const int l = S.lanef();
+    double wn[WR];
+#pragma unroll
+    for (int j = 0; j < WR; ++j) {
+      const int i = l + j * WAVE;
+      wn[j] = i < nw ? wb[i + 6 < nw ? i + 6 : i] : 0.0;
+    }
+    double pv = l < 11 ? pb[l] : 0.0;
+    const double u0 = l < 6 ? wb[l] : 0.0;
+    if (lp.x_hist && l < 8) lp.x_hist[(kb + b) * 8 + l] = pv;
+    if (lp.u_hist && l < 6) lp.u_hist[(kb + b) * 6 + l] = u0;
+    const double th = readlane_d(pv, 3), ps = readlane_d(pv, 4), xs2 = readlane_d(pv, 10);
+    const double v = readlane_d(u0, 0);
+    // x0 <- x0 + T f(x0, u0): [v c(psi) c(th), v s(psi) c(th), v s(th), u1..u5]
+    const double ush = __shfl(u0, l >= 3 && l < 8 ? l - 2 : 0, WAVE);
+    double fx = 0.0;
+    if (l == 0) fx = v * cos(ps) * cos(th);
+    else if (l == 1) fx = v * sin(ps) * cos(th);
+    else if (l == 2) fx = v * sin(th);
+    else if (l < 8) fx = ush;
+    else if (l == 8) fx = lp.vt[b] * cos(xs2);
+    else if (l == 9) fx = lp.vt[b] * sin(xs2);
+    else if (l == 10) fx = lp.wt[b];
+    sync();
+    if (l < 11) pb[l] = pv + T * fx;
+#pragma unroll
+    for (int j = 0; j < WR; ++j) {
+      const int i = l + j * WAVE;
+      if (i < nw) wb[i] = wn[j];
+    }
+    (void)N;
+    sync();
+  }
+}
+
 // closed-loop shift kernel (Python/NMPC_TT.py:13-30): one thread per scenario
 __global__ void nmpc_shift_kernel(int B, int N, int np, double T, double* p, long long ld_p,
                                   const double* u, double* w_out, const double* vt, const double* wt) {
@@ -1727,6 +1807,7 @@ int fail(int code, const std::string& msg) {
 }  // namespace
 
 typedef void (*KernFn)(const Params*, int, IO);
+typedef void (*LoopFn)(const Params*, int, IO, Loop);
 
 struct nmpc_handle {
   Params hp;
@@ -1739,6 +1820,7 @@ struct nmpc_handle {
   int* ibuf = nullptr;
   size_t ibuf_bytes = 0;
   KernFn kern = nullptr;
+  LoopFn loop = nullptr;
   int ws_doubles = 0;
   bool trace = false;
   double* dtrace = nullptr;
@@ -1752,14 +1834,27 @@ using CapA = Cap<20, 15>;   // BASELINE configs 2-4 (N=20, <=10 obstacles) and t
 using CapB = Cap<31, 21>;
 using CapC = Cap<63, 21>;   // any supported shape
 
-static void pick_class(const Params& P, KernFn* fn, int* lds_doubles, int* ws_doubles) {
-  if (P.N <= CapA::nmax && P.m <= CapA::mmax) {
-    *fn = nmpc_solve_kernel<CapA>; *lds_doubles = CapA::L.total; *ws_doubles = CapA::L.wstotal;
-  } else if (P.N <= CapB::nmax && P.m <= CapB::mmax) {
-    *fn = nmpc_solve_kernel<CapB>; *lds_doubles = CapB::L.total; *ws_doubles = CapB::L.wstotal;
-  } else {
-    *fn = nmpc_solve_kernel<CapC>; *lds_doubles = CapC::L.total; *ws_doubles = CapC::L.wstotal;
+template <class CAP>
+static void set_class(KernFn* fn, LoopFn* lfn, int* lds_doubles, int* ws_doubles) {
+  *fn = nmpc_solve_kernel<CAP>; *lfn = nmpc_closed_loop_kernel<CAP>;
+  *lds_doubles = CAP::L.total; *ws_doubles = CAP::L.wstotal;
+}
+
+static void pick_class(const Params& P, KernFn* fn, LoopFn* lfn, int* lds_doubles, int* ws_doubles) {
+  if (P.N <= CapA::nmax && P.m <= CapA::mmax) set_class<CapA>(fn, lfn, lds_doubles, ws_doubles);
+  else if (P.N <= CapB::nmax && P.m <= CapB::mmax) set_class<CapB>(fn, lfn, lds_doubles, ws_doubles);
+  else set_class<CapC>(fn, lfn, lds_doubles, ws_doubles);
+}
+
+static int ensure_ws(nmpc_handle* h, int B) {
+  const size_t need = (size_t)B * h->ws_doubles * sizeof(double);
+  if (need > h->ws_bytes) {
+    if (h->dws) hipFree(h->dws);
+    h->dws = nullptr; h->ws_bytes = 0;
+    if (hipMalloc(&h->dws, need) != hipSuccess) return fail(NMPC_E_NOMEM, "hipMalloc workspace");
+    h->ws_bytes = need;
   }
+  return NMPC_OK;
 }
 
 extern "C" {
@@ -1814,7 +1909,7 @@ int nmpc_create(const nmpc_desc* desc, nmpc_handle** out) {
   P.o = desc->opts;
   {
     int ldsd = 0;
-    pick_class(P, &h->kern, &ldsd, &h->ws_doubles);
+    pick_class(P, &h->kern, &h->loop, &ldsd, &h->ws_doubles);
     h->lds_bytes = ldsd * 8;
   }
   if (h->lds_bytes > 160 * 1024) {
@@ -1827,6 +1922,8 @@ int nmpc_create(const nmpc_desc* desc, nmpc_handle** out) {
     hipFree(h->dprm); delete h; return fail(NMPC_E_HIP, "hipMemcpy params");
   }
   if (hipFuncSetAttribute((const void*)h->kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                          h->lds_bytes) != hipSuccess ||
+      hipFuncSetAttribute((const void*)h->loop, hipFuncAttributeMaxDynamicSharedMemorySize,
                           h->lds_bytes) != hipSuccess) {
     hipFree(h->dprm); delete h; return fail(NMPC_E_HIP, "hipFuncSetAttribute(MaxDynamicSharedMemorySize)");
   }
@@ -1906,16 +2003,8 @@ int nmpc_solve_batch_dev(nmpc_handle* h, int32_t B, const double* x0, int64_t ld
     hipMemsetAsync(h->dtrace, 0, need, (hipStream_t)stream);
     io.trace = h->dtrace;
   }
-  {
-    const size_t need = (size_t)B * h->ws_doubles * sizeof(double);
-    if (need > h->ws_bytes) {
-      if (h->dws) hipFree(h->dws);
-      h->dws = nullptr; h->ws_bytes = 0;
-      if (hipMalloc(&h->dws, need) != hipSuccess) return fail(NMPC_E_NOMEM, "hipMalloc workspace");
-      h->ws_bytes = need;
-    }
-    io.ws = h->dws;
-  }
+  if (int rc = ensure_ws(h, B)) return rc;
+  io.ws = h->dws;
   h->last_B = B;
   hipLaunchKernelGGL(h->kern, dim3(B), dim3(WAVE), h->lds_bytes, (hipStream_t)stream,
                      (const Params*)h->dprm, (int)B, io);
@@ -2003,6 +2092,37 @@ int nmpc_shift_dev(nmpc_handle* h, int32_t B, double* p, int64_t ld_p, const dou
                      h->hp.N, h->hp.np, h->hp.T, p, (long long)ld_p, u_sol, w_out, v_t, w_t);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return fail(NMPC_E_HIP, std::string("shift launch: ") + hipGetErrorString(e));
+  return NMPC_OK;
+}
+
+int nmpc_closed_loop_dev(nmpc_handle* h, int32_t B, int32_t K, const double* lbx, int64_t ld_lbx,
+                         const double* ubx, int64_t ld_ubx, const double* lbg, int64_t ld_lbg,
+                         const double* ubg, int64_t ld_ubg, double* p, int64_t ld_p, double* w,
+                         const double* v_t, const double* w_t, double* u_hist, double* x_hist,
+                         double* f_hist, int32_t* status_hist, int32_t* iters_hist, void* stream) {
+  if (!h) return fail(NMPC_E_INVALID, "null handle");
+  if (B < 0 || K < 0) return fail(NMPC_E_INVALID, "B < 0 or K < 0");
+  if (B == 0 || K == 0) return NMPC_OK;
+  if (!lbx || !ubx || !lbg || !ubg || !p || !w || !v_t || !w_t)
+    return fail(NMPC_E_INVALID, "required pointer is null");
+  const Params& P = h->hp;
+  if ((ld_lbx != 0 && ld_lbx < P.nw) || (ld_ubx != 0 && ld_ubx < P.nw) || (ld_lbg != 0 && ld_lbg < P.ng) ||
+      (ld_ubg != 0 && ld_ubg < P.ng) || ld_p < P.np)
+    return fail(NMPC_E_INVALID, "leading dimension smaller than the vector length");
+  if ((long long)B * K > (1LL << 40)) return fail(NMPC_E_INVALID, "B*K too large");
+  IO io;
+  std::memset(&io, 0, sizeof(io));
+  io.lbx = lbx; io.ubx = ubx; io.lbg = lbg; io.ubg = ubg;
+  io.ld_lbx = ld_lbx; io.ld_ubx = ld_ubx; io.ld_lbg = ld_lbg; io.ld_ubg = ld_ubg;
+  if (int rc = ensure_ws(h, B)) return rc;
+  io.ws = h->dws;
+  Loop lp;
+  lp.K = K; lp.p = p; lp.ld_p = ld_p; lp.w = w; lp.vt = v_t; lp.wt = w_t;
+  lp.u_hist = u_hist; lp.x_hist = x_hist; lp.f_hist = f_hist; lp.st_hist = status_hist; lp.it_hist = iters_hist;
+  hipLaunchKernelGGL(h->loop, dim3(B), dim3(WAVE), h->lds_bytes, (hipStream_t)stream,
+                     (const Params*)h->dprm, (int)B, io, lp);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return fail(NMPC_E_HIP, std::string("closed-loop launch: ") + hipGetErrorString(e));
   return NMPC_OK;
 }
 

@@ -222,6 +222,49 @@ class Solver:
                                     C.c_void_p(v_t.data_ptr()), C.c_void_p(w_t.data_ptr()),
                                     C.c_void_p(stream.cuda_stream)))
 
+    def closed_loop_device(self, K: int, lbx, ubx, lbg, ubg, p, w, v_t, w_t, hist: dict | None = None,
+                           stream=None):
+        """K closed-loop MPC steps per scenario in one launch (see nmpc_closed_loop_dev).
+
+        p (B,np) and w (B,nw) are advanced in place; ``hist`` may hold device
+        tensors u (K,B,6), x (K,B,8), f (K,B), status/iters (K,B) int32.
+        """
+        import torch
+
+        L = _lib.lib()
+        B = w.shape[0]
+        hist = hist or {}
+
+        def dv(t, n):
+            assert t.dtype == torch.float64 and t.is_cuda and t.is_contiguous()
+            if t.dim() == 1:
+                assert t.shape[0] == n
+                return C.c_void_p(t.data_ptr()), 0
+            assert t.shape == (B, n), (tuple(t.shape), (B, n))
+            return C.c_void_p(t.data_ptr()), n
+
+        ins = []
+        for t, n in ((lbx, self.nw), (ubx, self.nw), (lbg, self.ng), (ubg, self.ng)):
+            ins += list(dv(t, n))
+        assert p.shape == (B, self.np) and p.is_contiguous() and p.dtype == torch.float64
+        assert w.shape == (B, self.nw) and w.is_contiguous() and w.dtype == torch.float64
+        for t, shp, dt in (("u", (K, B, 6), torch.float64), ("x", (K, B, 8), torch.float64),
+                           ("f", (K, B), torch.float64), ("status", (K, B), torch.int32),
+                           ("iters", (K, B), torch.int32)):
+            if hist.get(t) is not None:
+                assert tuple(hist[t].shape) == shp and hist[t].dtype == dt and hist[t].is_contiguous(), t
+
+        def op(k):
+            t = hist.get(k)
+            return C.c_void_p(t.data_ptr()) if t is not None else C.c_void_p(0)
+
+        if stream is None:
+            stream = torch.cuda.current_stream()
+        _lib.check(L.nmpc_closed_loop_dev(self._h, B, K, *ins, C.c_void_p(p.data_ptr()), self.np,
+                                          C.c_void_p(w.data_ptr()), C.c_void_p(v_t.data_ptr()),
+                                          C.c_void_p(w_t.data_ptr()), op("u"), op("x"), op("f"),
+                                          op("status"), op("iters"), C.c_void_p(stream.cuda_stream)))
+
     def set_trace(self, enable: bool):
         _lib.check(_lib.lib().nmpc_set_trace(self._h, int(enable)))
 

@@ -280,3 +280,86 @@ def test_shift_kernel_matches_reference_shift():
         np.testing.assert_allclose(p[b, :8].cpu().numpy(), x1, rtol=1e-15, atol=1e-12)
         np.testing.assert_allclose(p[b, 8:11].cpu().numpy(), xs1, rtol=1e-15, atol=1e-12)
         np.testing.assert_array_equal(w[b].cpu().numpy(), u1.T.ravel())
+
+
+def _closed_loop_inputs(spec, B, seed):
+    import torch
+    from nmpc_amd import draw_scenarios
+
+    f64 = dict(dtype=torch.float64, device="cuda")
+    P = draw_scenarios(spec, B, seed=seed)
+    bnd = [torch.tensor(v, **f64) for v in spec.bounds()]
+    return P, bnd, torch.full((B,), 12.0, **f64), torch.full((B,), 0.01, **f64)
+
+
+def test_closed_loop_kernel_matches_per_step_launches():
+    """nmpc_closed_loop_dev (K steps in one launch) == K x (solve_batch_dev + shift_dev)."""
+    import torch
+    from nmpc_amd import make_spec
+
+    spec = make_spec("race_track_2", N=20, T=0.2)
+    B, K = 96, 4
+    P, bnd, vt, wt = _closed_loop_inputs(spec, B, 1003)
+    f64 = dict(dtype=torch.float64, device="cuda")
+    s = _solver(spec)
+    # per-step launches
+    p1 = torch.tensor(P, **f64)
+    w1 = torch.zeros(B, spec.nw, **f64)
+    out = {"x": torch.empty(B, spec.nw, **f64), "f": torch.empty(B, **f64),
+           "status": torch.empty(B, dtype=torch.int32, device="cuda"),
+           "iters": torch.empty(B, dtype=torch.int32, device="cuda")}
+    ref = {"u": [], "x": [], "f": [], "status": [], "iters": []}
+    for _ in range(K):
+        ref["x"].append(p1[:, :8].clone())
+        s.solve_device(w1, *bnd, p1, out)
+        ref["u"].append(out["x"][:, :6].clone())
+        for k in ("f", "status", "iters"):
+            ref[k].append(out[k].clone())
+        s.shift_device(p1, out["x"], w1, vt, wt)
+    # one launch
+    p2 = torch.tensor(P, **f64)
+    w2 = torch.zeros(B, spec.nw, **f64)
+    hist = {"u": torch.empty(K, B, 6, **f64), "x": torch.empty(K, B, 8, **f64), "f": torch.empty(K, B, **f64),
+            "status": torch.empty(K, B, dtype=torch.int32, device="cuda"),
+            "iters": torch.empty(K, B, dtype=torch.int32, device="cuda")}
+    s.closed_loop_device(K, *bnd, p2, w2, vt, wt, hist)
+    torch.cuda.synchronize()
+    for k in ("status", "iters"):
+        np.testing.assert_array_equal(hist[k].cpu().numpy(), torch.stack(ref[k]).cpu().numpy(), err_msg=k)
+    for k in ("u", "x", "f"):
+        a, b_ = hist[k].cpu().numpy(), torch.stack(ref[k]).cpu().numpy()
+        assert _rel(a, b_) <= 1e-12, (k, _rel(a, b_))
+    assert _rel(p2.cpu().numpy(), p1.cpu().numpy()) <= 1e-12
+    assert _rel(w2.cpu().numpy(), w1.cpu().numpy()) <= 1e-12
+
+
+def test_closed_loop_parity_with_oracle_loop():
+    """The fused closed loop against the oracle's own solve + shift_timestep loop
+    (Python/NMPC_TT.py:348-402 restated): same statuses and applied controls."""
+    import torch
+    from nmpc_amd import make_spec
+
+    spec = make_spec("race_track_2", N=10, T=0.2)
+    B, K = 3, 3
+    P, bnd, vt, wt = _closed_loop_inputs(spec, B, 21)
+    f64 = dict(dtype=torch.float64, device="cuda")
+    s = _solver(spec)
+    p = torch.tensor(P, **f64)
+    w = torch.zeros(B, spec.nw, **f64)
+    hist = {"u": torch.empty(K, B, 6, **f64), "x": torch.empty(K, B, 8, **f64),
+            "status": torch.empty(K, B, dtype=torch.int32, device="cuda")}
+    s.closed_loop_device(K, *bnd, p, w, vt, wt, hist)
+    torch.cuda.synchronize()
+    prob, ref = _oracle("race_track_2", 10, 0.2)
+    lbx, ubx, lbg, ubg = spec.bounds()
+    for b in range(B):
+        x0, xs, u0 = P[b, :8].copy(), P[b, 8:11].copy(), np.zeros(spec.nw)
+        for k in range(K):
+            np.testing.assert_allclose(hist["x"][k, b].cpu().numpy(), x0, rtol=1e-9, atol=1e-9)
+            r = ref.solve(u0, lbx, ubx, lbg, ubg, np.concatenate([x0, xs]))
+            assert int(hist["status"][k, b]) == r["status"], (b, k)
+            if r["status"] != 0:
+                break
+            assert _rel(hist["u"][k, b].cpu().numpy(), r["x"][:6]) <= TOL
+            x0, u1, xs = orc.shift_timestep(prob, x0, r["x"].reshape(spec.N, 6).T, xs)
+            u0 = u1.T.ravel()
