@@ -47,46 +47,75 @@ def survey_bytes_per_step(spec, ibar):
     return ibar * b_iter + io, s_stage, b_iter, io
 
 
-def pmc_traffic(kernel="nmpc_closed_loop_kernel"):
-    """HBM bytes per launch of `kernel` from the newest committed rocprofv3 PMC pass
-    (profiles/r*_pmc_fetch_write.csv): FETCH_SIZE is doubled per the gfx950
-    correction (MI355X_MICROARCH.md, HBM section), WRITE_SIZE taken as is; KB -> B."""
+def pmc_traffic(kernel, steps, batch):
+    """HBM bytes per launch of `kernel` from the newest committed rocprofv3 PMC
+    summary (profiles/r*_pmc.csv, written by scripts/rocpd_summary.py --csv from
+    the FETCH_SIZE / WRITE_SIZE passes of scripts/profile_round.sh): FETCH_SIZE
+    doubled per the gfx950 correction (MI355X_MICROARCH.md, HBM section),
+    WRITE_SIZE as is, KB -> B.  Only used when the profiled launch had the same
+    steps and batch as this run."""
     import csv
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_fetch_write.csv")))
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc.csv")))
     if not files:
         return None, None
-    fetch, write = [], []
+    vals = {}
     for row in csv.DictReader(open(files[-1])):
-        if kernel not in row.get("Kernel_Name", ""):
-            continue
-        (fetch if row["Counter_Name"] == "FETCH_SIZE" else write).append(float(row["Counter_Value"]))
-    if not fetch or not write:
+        if kernel in row["kernel"] and row.get("steps", "") == str(steps) and row.get("batch", "") == str(batch):
+            vals[row["counter"]] = float(row["value"])
+    if "FETCH_SIZE" not in vals or "WRITE_SIZE" not in vals:
         return None, None
-    return (2.0 * np.mean(fetch) + np.mean(write)) * 1024.0, os.path.relpath(files[-1], ROOT)
+    return (2.0 * vals["FETCH_SIZE"] + vals["WRITE_SIZE"]) * 1024.0, os.path.relpath(files[-1], ROOT)
 
 
-def cpu_baseline(spec_cfg, P, lbx, ubx, lbg, ubg, budget_s=15.0):
-    """Time the CPU oracle (numpy dense IPOPT restatement, 1 core) on a bounded
-    sample of the same scenarios (cold start)."""
+def _cpu_worker(args):
+    """Solve scenarios rows[i::nproc] cold (u=0) with the oracle until the budget runs out."""
+    i, nproc, layout, N, T, P, lbx, ubx, lbg, ubg, budget_s = args
+    import warnings
+    from threadpoolctl import threadpool_limits
+
+    threadpool_limits(1)  # one core per worker process
+    warnings.filterwarnings("ignore", category=RuntimeWarning)  # -inf bounds in the initial-point push
     sys.path.insert(0, ROOT)
     from oracle import nmpc_oracle as orc
 
-    layout = "race_track_2" if spec_cfg.n_obs == 10 else (None if spec_cfg.n_obs == 0 else "nmpc_tt")
-    prob = orc.make_problem(layout, N=spec_cfg.N, T=spec_cfg.T)
-    solver = orc.IpoptDense(prob, orc.REFERENCE_OPTS)
+    solver = orc.IpoptDense(orc.make_problem(layout, N=N, T=T), orc.REFERENCE_OPTS)
     t0 = time.perf_counter()
-    n = 0
-    iters = 0
-    while n < P.shape[0] and (time.perf_counter() - t0) < budget_s:
-        r = solver.solve(np.zeros(spec_cfg.nw), lbx, ubx, lbg, ubg, P[n])
+    n = iters = 0
+    for row in range(i, P.shape[0], nproc):
+        if time.perf_counter() - t0 >= budget_s:
+            break
+        r = solver.solve(np.zeros(6 * N), lbx, ubx, lbg, ubg, P[row])
         iters += r["iter"]
         n += 1
-    el = time.perf_counter() - t0
-    return {"value": n / el, "unit": "MPC steps/s", "cores": 1, "kind": "port",
-            "sample": f"{n} cold-start solves of the first {n} config-3 scenarios by "
-                      f"oracle/nmpc_oracle.py (numpy, dense single-shooting IPOPT restatement) "
-                      f"in {el:.1f}s, mean {iters / max(n, 1):.1f} iterations"}
+    return n, iters, time.perf_counter() - t0
+
+
+def cpu_baseline(spec_cfg, P, lbx, ubx, lbg, ubg, budget_s=15.0):
+    """Time the CPU oracle (numpy dense IPOPT restatement, oracle/nmpc_oracle.py)
+    on a bounded sample of the same scenarios (cold start), one scenario per
+    worker process at a time (scenarios split across processes).
+    Must run before this process touches the GPU (the workers are forked)."""
+    import multiprocessing as mp
+
+    try:
+        ncpu = len(os.sched_getaffinity(0))
+    except AttributeError:
+        ncpu = os.cpu_count() or 1
+    nproc = max(1, min(16, ncpu))  # the GPU box's CPU share is 16
+    layout = "race_track_2" if spec_cfg.n_obs == 10 else (None if spec_cfg.n_obs == 0 else "nmpc_tt")
+    sample = P[: nproc * 64]
+    t0 = time.perf_counter()
+    with mp.get_context("fork").Pool(nproc) as pool:
+        res = pool.map(_cpu_worker, [(i, nproc, layout, spec_cfg.N, spec_cfg.T, sample, lbx, ubx, lbg, ubg,
+                                      budget_s) for i in range(nproc)])
+    wall = time.perf_counter() - t0
+    n = sum(r[0] for r in res)
+    iters = sum(r[1] for r in res)
+    return {"value": n / wall, "unit": "MPC steps/s", "cores": nproc, "kind": "port",
+            "sample": f"{n} cold-start solves (u=0) of config-{3 if spec_cfg.n_obs == 10 else '?'} scenarios by "
+                      f"oracle/nmpc_oracle.py (numpy dense single-shooting IPOPT restatement), {nproc} worker "
+                      f"processes x ~{budget_s:.0f}s, wall {wall:.1f}s, mean {iters / max(n, 1):.1f} iterations"}
 
 
 def main():
@@ -112,13 +141,18 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+
+    spec = config_spec(args.config)
+    B, K, W = args.batch, args.steps, args.warmup
+    cpu_res = None
+    if world == 1 and not args.no_cpu_baseline:  # forks workers: before the GPU is initialised
+        lb = spec.bounds()
+        cpu_res = cpu_baseline(spec, draw_scenarios(spec, B, seed=1000 + args.config), *lb,
+                               budget_s=args.cpu_budget)
     if world > 1:
         torch.cuda.set_device(local_rank)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
     dev = torch.device("cuda", local_rank if world > 1 else 0)
-
-    spec = config_spec(args.config)
-    B, K, W = args.batch, args.steps, args.warmup
     # global scenario stream, sliced per rank (results independent of world size)
     P_all = draw_scenarios(spec, B * world, seed=1000 + args.config)
     P = P_all[shard(B * world, world, rank)]
@@ -135,7 +169,7 @@ def main():
     stream = torch.cuda.current_stream()
 
     def hist_bufs(k):
-        return {"u": torch.empty(k, B, 6, **f64), "f": torch.empty(k, B, **f64),
+        return {"u": torch.empty(k, B, 6, **f64), "f": torch.empty(k, B, **f64), "fov": torch.zeros(k, B, **f64),
                 "status": torch.empty(k, B, **i32), "iters": torch.empty(k, B, **i32)}
 
     out = {"x": torch.empty(B, spec.nw, **f64), "f": torch.empty(B, **f64),
@@ -201,9 +235,11 @@ def main():
             dist.all_reduce(tot, op=dist.ReduceOp.SUM)
         sts = ht["status"].cpu().numpy()
         hist = {int(s_): int((sts == s_).sum()) for s_ in np.unique(sts)}
+        timed_run.fov = float(ht["fov"].mean().item())
         return float(el_t.item()), kern_ms, float(tot[0].item() / tot[1].item()), hist
 
     elapsed, kern_ms, ibar, status_hist = timed_run(args.mode, p0.clone(), w0.clone())
+    fov_mean = timed_run.fov if args.mode == "fused" else None
     side = None
     if args.mode == "fused" and not args.no_per_step:
         e2, km2, ib2, h2 = timed_run("per_step", p0.clone(), w0.clone())
@@ -221,9 +257,10 @@ def main():
         steps_per_launch = K if args.mode == "fused" else 1
         kname = "nmpc_closed_loop_kernel" if args.mode == "fused" else "nmpc_solve_kernel"
         flops_launch = B * steps_per_launch * ibar * (spec.N + 1) * KFLOP_PER_STAGE_ITER * 1e3
-        achieved = flops_launch / kern_avg_s / 1e12
+        achieved_tf = flops_launch / kern_avg_s / 1e12
         bps, s_stage, b_iter, io = survey_bytes_per_step(spec, ibar)
-        traffic, traffic_src = pmc_traffic(kname)
+        achieved_gbs = B * steps_per_launch * bps / kern_avg_s / 1e9
+        traffic, traffic_src = pmc_traffic(kname, K if args.mode == "fused" else None, B)
         mode_txt = {"fused": f"{K} warm-started closed-loop MPC steps per scenario in one launch",
                     "per_step": "warm-started closed-loop MPC steps, one launch per step",
                     "cold": "cold-start (u=0) solves, one launch per step"}[args.mode]
@@ -235,24 +272,27 @@ def main():
             "config": {"workload": f"config {args.config}: batch={B}/GPU, N={spec.N}, {spec.n_obs} static "
                                    f"obstacles (Race Track 2.py), T={spec.T}, reference IPOPT opts, {mode_txt}",
                        "global_batch": B * world, "seq_len": spec.N, "parallelism": f"dp{world}"},
-            "roofline": {"bound": "mfma", "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
-                         "frac": achieved / FP64_PEAK_TFLOPS, "traffic": traffic,
-                         "traffic_unit": "HBM bytes per launch (2*FETCH_SIZE + WRITE_SIZE)",
+            "roofline": {"bound": "hbm", "achieved": achieved_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved_gbs / HBM_PEAK_GBS, "traffic": traffic,
+                         "traffic_unit": "HBM bytes per launch (2*FETCH_SIZE + WRITE_SIZE, rocprofv3 PMC)",
                          "traffic_source": traffic_src,
                          "kernel": kname, "kernel_avg_ms": kern_avg_s * 1e3, "launches": n_launch,
-                         "model": f"SURVEY 8(d) {KFLOP_PER_STAGE_ITER} kflop/stage-iteration x (N+1) x "
-                                  f"I_bar={ibar:.2f} x B x {steps_per_launch} step(s) per launch; "
-                                  f"FP64 peak (vector = matrix)"},
-            "survey_hbm_model": {"bytes_per_step": bps, "S_stage": s_stage, "B_iter": b_iter, "IO": io,
-                                 "equivalent_GBs": B * steps_per_launch * bps / kern_avg_s / 1e9,
-                                 "io_only_GBs": B * steps_per_launch * io / kern_avg_s / 1e9},
+                         "model": f"SURVEY 8(d) streamed-KKT bytes: I_bar x B_iter + IO = {bps:.0f} B per "
+                                  f"MPC step (I_bar={ibar:.2f}, B_iter={b_iter} B, IO={io} B) x B={B} x "
+                                  f"{steps_per_launch} step(s) per launch / kernel time",
+                         "fp64": {"achieved_tflops": achieved_tf, "peak_tflops": FP64_PEAK_TFLOPS,
+                                  "frac": achieved_tf / FP64_PEAK_TFLOPS,
+                                  "model": f"{KFLOP_PER_STAGE_ITER} kflop/stage-iteration x (N+1) x I_bar"},
+                         "io_only_GBs": B * steps_per_launch * io / kern_avg_s / 1e9},
             "mean_ip_iterations": ibar,
             "status_histogram": status_hist,
         }
+        if fov_mean is not None:
+            res["closed_loop_fov_error_mean_m"] = fov_mean  # Python/NMPC_TT.py:433-437 metric, per step
         if side is not None:
             res["per_step_launch"] = side
-        if world == 1 and not args.no_cpu_baseline:
-            res["cpu_baseline"] = cpu_baseline(spec, P, lbx, ubx, lbg, ubg, budget_s=args.cpu_budget)
+        if cpu_res is not None:
+            res["cpu_baseline"] = cpu_res
         print(json.dumps(res))
     if world > 1:
         dist.destroy_process_group()

@@ -157,17 +157,22 @@ int nmpc_shift_dev(nmpc_handle* h, int32_t B, double* p, int64_t ld_p,
  * wavefront, so no step waits for another scenario's slowest solve.  Step k
  * solves with x0 = w (warm start) and p, records x0 = p[0:8] (x_hist), the
  * applied control u0 = x[0:6] (u_hist), f, status and iterations, then applies
- * x0 <- x0 + T f(x0,u0), w <- [u(:,2:N), u(:,N)], xs <- unicycle step with
- * (v_t, w_t) exactly as nmpc_shift_dev.  DEVICE pointers, enqueued on `stream`.
+ * x0 <- x0 + T f(x0,u0), w <- [u(:,2:N), u(:,N)], xs <- xs + T [v cos, v sin, w]
+ * with the target controls (v, w) = (v_t, w_t)[k*ld_tk + b*ld_tb] (the
+ * scripts' con_t schedules: ld_tk = 1, ld_tb = 0 for one shared schedule;
+ * ld_tk = 0 for constant controls), and records the FOV-centre error
+ * |FOV(x0_{k+1}) - xs_k[0:2]| (Python/NMPC_TT.py:397-400,433-437) in fov_hist.
+ * DEVICE pointers, enqueued on `stream`.
  *   p   : np x B (ld_p >= np), in/out (advanced K steps)
  *   w   : nw x B (ld nw), in: first warm start; out: the last step's shifted solution
- *   u_hist K x B x 6, x_hist K x B x 8, f_hist / status_hist / iters_hist K x B;
- *   each nullable.  Bounds as in nmpc_solve_batch_dev. */
+ *   u_hist K x B x 6, x_hist K x B x 8, f_hist / fov_hist / status_hist /
+ *   iters_hist K x B; each nullable.  Bounds as in nmpc_solve_batch_dev. */
 int nmpc_closed_loop_dev(nmpc_handle* h, int32_t B, int32_t K,
                          const double* lbx, int64_t ld_lbx, const double* ubx, int64_t ld_ubx,
                          const double* lbg, int64_t ld_lbg, const double* ubg, int64_t ld_ubg,
-                         double* p, int64_t ld_p, double* w, const double* v_t, const double* w_t,
-                         double* u_hist, double* x_hist, double* f_hist,
+                         double* p, int64_t ld_p, double* w,
+                         const double* v_t, const double* w_t, int64_t ld_tk, int64_t ld_tb,
+                         double* u_hist, double* x_hist, double* f_hist, double* fov_hist,
                          int32_t* status_hist, int32_t* iters_hist, void* stream);
 
 const char* nmpc_last_error(void);

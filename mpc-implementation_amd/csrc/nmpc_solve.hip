@@ -102,6 +102,11 @@ struct Cap {
   static constexpr Lay L = make_layout(NMAX, MMAX);
 };
 
+// waves per SIMD the kernels are register-budgeted for (256 VGPRs at 2)
+#ifndef NMPC_WAVES_PER_EU
+#define NMPC_WAVES_PER_EU 2
+#endif
+
 struct IO {
   const double *x0, *lbx, *ubx, *lbg, *ubg, *p;
   long long ld_x0, ld_lbx, ld_ubx, ld_lbg, ld_ubg, ld_p;
@@ -634,8 +639,8 @@ struct Solver {
   // cost-to-go matrix, three LDS exchanges per stage:
   //   (1) A^T P A (register), S~ = S + B^T P A and R~ = R + B^T P B (21 lanes)
   //       straight from P (A = I + E, B = [b0 | T e_3..7]);
-  //   (2) every lanef(): Cholesky of R~ (inertia: all pivots > 0), R~^{-1};
-  //       lanes 0..7: column j of K = -R~^{-1} S~, lanef() 8: k = -R~^{-1} r~;
+  //   (2) every lanef(): Cholesky of R~ (inertia: all pivots > 0); lanes 0..7:
+  //       column j of K = -R~^{-1} S~, lanef() 8: k = -R~^{-1} r~ (two triangular solves);
   //   (3) P_k = Q_k + A^T P A + S~^T K ; p_k = q_k + A^T p + K^T r~.
   // Stores K_k, k_k and R~_k (for the gradient-only re-solve).
   __device__ __forceinline__ bool riccati(const GLB double* Rd, const GLB double* rv) {
@@ -730,43 +735,31 @@ struct Solver {
             Lm[r * (r + 1) / 2 + c] = v * ig;
           }
         }
-        // L^{-1} (packed lower) and R~^{-1} = L^{-T} L^{-1} (packed lower)
-        double Li[21], Rv[21];
-#pragma unroll
-        for (int c = 0; c < 6; ++c) {
-          Li[c * (c + 1) / 2 + c] = idg[c];
-#pragma unroll
-          for (int r = c + 1; r < 6; ++r) {
-            double a = 0.0;
-#pragma unroll
-            for (int t = c; t < r; ++t) a += Lm[r * (r + 1) / 2 + t] * Li[t * (t + 1) / 2 + c];
-            Li[r * (r + 1) / 2 + c] = -idg[r] * a;
-          }
-        }
-#pragma unroll
-        for (int r = 0; r < 6; ++r) {
-#pragma unroll
-          for (int c = 0; c <= r; ++c) {
-            double a = 0.0;
-#pragma unroll
-            for (int t = r; t < 6; ++t) a += Li[t * (t + 1) / 2 + r] * Li[t * (t + 1) / 2 + c];
-            Rv[r * (r + 1) / 2 + c] = a;
-          }
-        }
         rt[0] = rv[k * 6 + 0] + ((b00 * pc[0] + b10 * pc[1]) + b20 * pc[2]);
 #pragma unroll
         for (int r = 1; r < 6; ++r) rt[r] = rv[k * 6 + r] + T * pc[2 + r];
         if (lanef() < 9) {
-          double col[6];
-#pragma unroll
-          for (int r = 0; r < 6; ++r) col[r] = (lanef() < 8) ? St[r * 8 + lanef()] : rt[r];
+          // column lanef() of K = -R~^{-1} S~ (lane 8: k = -R~^{-1} r~) by two
+          // triangular solves with the Cholesky factor
+          double v[6];
 #pragma unroll
           for (int r = 0; r < 6; ++r) {
-            double a = 0.0;
+            double a = (lanef() < 8) ? St[r * 8 + lanef()] : rt[r];
 #pragma unroll
-            for (int c = 0; c < 6; ++c) a += Rv[r >= c ? r * (r + 1) / 2 + c : c * (c + 1) / 2 + r] * col[c];
-            if (lanef() < 8) { Kc[r * 8 + lanef()] = -a; K[k * 48 + r * 8 + lanef()] = -a; }
-            else kf[k * 6 + r] = -a;
+            for (int t = 0; t < r; ++t) a -= Lm[r * (r + 1) / 2 + t] * v[t];
+            v[r] = a * idg[r];
+          }
+#pragma unroll
+          for (int r = 5; r >= 0; --r) {
+            double a = v[r];
+#pragma unroll
+            for (int t = r + 1; t < 6; ++t) a -= Lm[t * (t + 1) / 2 + r] * v[t];
+            v[r] = a * idg[r];
+          }
+#pragma unroll
+          for (int r = 0; r < 6; ++r) {
+            if (lanef() < 8) { Kc[r * 8 + lanef()] = -v[r]; K[k * 48 + r * 8 + lanef()] = -v[r]; }
+            else kf[k * 6 + r] = -v[r];
           }
         }
         sync();
@@ -1688,7 +1681,7 @@ __device__ __forceinline__ void solve_one(Solver<CAP>& S, const Params* __restri
 }
 
 template <class CAP>
-__global__ __launch_bounds__(WAVE, 2) void nmpc_solve_kernel(const Params* __restrict__ prm, int B, IO io) {
+__global__ __launch_bounds__(WAVE, NMPC_WAVES_PER_EU) void nmpc_solve_kernel(const Params* __restrict__ prm, int B, IO io) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   const int b = blockIdx.x;
   if (b >= B) return;
@@ -1705,13 +1698,15 @@ struct Loop {
   double* p;          // np x B (ld_p), advanced in place
   long long ld_p;
   double* w;          // nw x B warm start, in/out (holds the shifted last solution on exit)
-  const double *vt, *wt;
+  const double *vt, *wt;             // target (v, w) for step k, scenario b: [k * ld_tk + b * ld_tb]
+  long long ld_tk, ld_tb;
   double *u_hist, *x_hist, *f_hist;  // K x B x 6, K x B x 8, K x B (nullable)
+  double* fov_hist;                  // K x B FOV-centre error (Python/NMPC_TT.py:397-400,433-437)
   int *st_hist, *it_hist;            // K x B (nullable)
 };
 
 template <class CAP>
-__global__ __launch_bounds__(WAVE, 2) void nmpc_closed_loop_kernel(const Params* __restrict__ prm, int B, IO io,
+__global__ __launch_bounds__(WAVE, NMPC_WAVES_PER_EU) void nmpc_closed_loop_kernel(const Params* __restrict__ prm, int B, IO io,
                                                                     Loop lp) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   const int b = blockIdx.x;
@@ -1757,11 +1752,23 @@ __global__ __launch_bounds__(WAVE, 2) void nmpc_closed_loop_kernel(const Params*
     else if (l == 1) fx = v * sin(ps) * cos(th);
     else if (l == 2) fx = v * sin(th);
     else if (l < 8) fx = ush;
-    else if (l == 8) fx = lp.vt[b] * cos(xs2);
-    else if (l == 9) fx = lp.vt[b] * sin(xs2);
-    else if (l == 10) fx = lp.wt[b];
+    else if (l == 8) fx = lp.vt[k * lp.ld_tk + b * lp.ld_tb] * cos(xs2);
+    else if (l == 9) fx = lp.vt[k * lp.ld_tk + b * lp.ld_tb] * sin(xs2);
+    else if (l == 10) fx = lp.wt[k * lp.ld_tk + b * lp.ld_tb];
     sync();
-    if (l < 11) pb[l] = pv + T * fx;
+    const double pnew = pv + T * fx;
+    if (l < 11) pb[l] = pnew;
+    if (lp.fov_hist) {
+      // FOV centre of the new state vs the target before its step
+      const double x1 = readlane_d(pnew, 0), y1 = readlane_d(pnew, 1), z1 = readlane_d(pnew, 2);
+      const double g5 = readlane_d(pnew, 5), g6 = readlane_d(pnew, 6);
+      const double xt = readlane_d(pv, 8), yt = readlane_d(pv, 9);
+      const double hv = prm->hv, hh = prm->hh;
+      const double ap = (z1 * tan(g6 + hv) - z1 * tan(g6 - hv)) / 2;
+      const double bp = (z1 * tan(g5 + hh) - z1 * tan(g5 - hh)) / 2;
+      const double xe = x1 + ap + z1 * tan(g6 - hv), ye = y1 + bp + z1 * tan(g5 - hh);
+      if (l == 0) lp.fov_hist[kb + b] = sqrt((xe - xt) * (xe - xt) + (ye - yt) * (ye - yt));
+    }
 #pragma unroll
     for (int j = 0; j < WR; ++j) {
       const int i = l + j * WAVE;
@@ -2098,13 +2105,15 @@ int nmpc_shift_dev(nmpc_handle* h, int32_t B, double* p, int64_t ld_p, const dou
 int nmpc_closed_loop_dev(nmpc_handle* h, int32_t B, int32_t K, const double* lbx, int64_t ld_lbx,
                          const double* ubx, int64_t ld_ubx, const double* lbg, int64_t ld_lbg,
                          const double* ubg, int64_t ld_ubg, double* p, int64_t ld_p, double* w,
-                         const double* v_t, const double* w_t, double* u_hist, double* x_hist,
-                         double* f_hist, int32_t* status_hist, int32_t* iters_hist, void* stream) {
+                         const double* v_t, const double* w_t, int64_t ld_tk, int64_t ld_tb,
+                         double* u_hist, double* x_hist, double* f_hist, double* fov_hist,
+                         int32_t* status_hist, int32_t* iters_hist, void* stream) {
   if (!h) return fail(NMPC_E_INVALID, "null handle");
   if (B < 0 || K < 0) return fail(NMPC_E_INVALID, "B < 0 or K < 0");
   if (B == 0 || K == 0) return NMPC_OK;
   if (!lbx || !ubx || !lbg || !ubg || !p || !w || !v_t || !w_t)
     return fail(NMPC_E_INVALID, "required pointer is null");
+  if (ld_tk < 0 || ld_tb < 0) return fail(NMPC_E_INVALID, "negative target-schedule stride");
   const Params& P = h->hp;
   if ((ld_lbx != 0 && ld_lbx < P.nw) || (ld_ubx != 0 && ld_ubx < P.nw) || (ld_lbg != 0 && ld_lbg < P.ng) ||
       (ld_ubg != 0 && ld_ubg < P.ng) || ld_p < P.np)
@@ -2117,8 +2126,9 @@ int nmpc_closed_loop_dev(nmpc_handle* h, int32_t B, int32_t K, const double* lbx
   if (int rc = ensure_ws(h, B)) return rc;
   io.ws = h->dws;
   Loop lp;
-  lp.K = K; lp.p = p; lp.ld_p = ld_p; lp.w = w; lp.vt = v_t; lp.wt = w_t;
-  lp.u_hist = u_hist; lp.x_hist = x_hist; lp.f_hist = f_hist; lp.st_hist = status_hist; lp.it_hist = iters_hist;
+  lp.K = K; lp.p = p; lp.ld_p = ld_p; lp.w = w; lp.vt = v_t; lp.wt = w_t; lp.ld_tk = ld_tk; lp.ld_tb = ld_tb;
+  lp.u_hist = u_hist; lp.x_hist = x_hist; lp.f_hist = f_hist; lp.fov_hist = fov_hist;
+  lp.st_hist = status_hist; lp.it_hist = iters_hist;
   hipLaunchKernelGGL(h->loop, dim3(B), dim3(WAVE), h->lds_bytes, (hipStream_t)stream,
                      (const Params*)h->dprm, (int)B, io, lp);
   const hipError_t e = hipGetLastError();

@@ -226,8 +226,10 @@ class Solver:
                            stream=None):
         """K closed-loop MPC steps per scenario in one launch (see nmpc_closed_loop_dev).
 
-        p (B,np) and w (B,nw) are advanced in place; ``hist`` may hold device
-        tensors u (K,B,6), x (K,B,8), f (K,B), status/iters (K,B) int32.
+        p (B,np) and w (B,nw) are advanced in place.  Target controls v_t, w_t:
+        (B,) per scenario, (1,) shared, (K,1) one schedule for all scenarios
+        (targets.schedule), or (K,B).  ``hist`` may hold device tensors
+        u (K,B,6), x (K,B,8), f (K,B), fov (K,B), status/iters (K,B) int32.
         """
         import torch
 
@@ -248,9 +250,17 @@ class Solver:
             ins += list(dv(t, n))
         assert p.shape == (B, self.np) and p.is_contiguous() and p.dtype == torch.float64
         assert w.shape == (B, self.nw) and w.is_contiguous() and w.dtype == torch.float64
+        assert v_t.shape == w_t.shape and v_t.dtype == torch.float64 and w_t.dtype == torch.float64
+        assert v_t.is_contiguous() and w_t.is_contiguous() and v_t.is_cuda and w_t.is_cuda
+        if v_t.dim() == 2:
+            assert v_t.shape[0] == K and v_t.shape[1] in (1, B), tuple(v_t.shape)
+            ld_tk, ld_tb = v_t.shape[1], (1 if v_t.shape[1] == B and B > 1 else 0)
+        else:
+            assert v_t.dim() == 1 and v_t.shape[0] in (1, B), tuple(v_t.shape)
+            ld_tk, ld_tb = 0, (1 if v_t.shape[0] == B and B > 1 else 0)
         for t, shp, dt in (("u", (K, B, 6), torch.float64), ("x", (K, B, 8), torch.float64),
-                           ("f", (K, B), torch.float64), ("status", (K, B), torch.int32),
-                           ("iters", (K, B), torch.int32)):
+                           ("f", (K, B), torch.float64), ("fov", (K, B), torch.float64),
+                           ("status", (K, B), torch.int32), ("iters", (K, B), torch.int32)):
             if hist.get(t) is not None:
                 assert tuple(hist[t].shape) == shp and hist[t].dtype == dt and hist[t].is_contiguous(), t
 
@@ -262,8 +272,9 @@ class Solver:
             stream = torch.cuda.current_stream()
         _lib.check(L.nmpc_closed_loop_dev(self._h, B, K, *ins, C.c_void_p(p.data_ptr()), self.np,
                                           C.c_void_p(w.data_ptr()), C.c_void_p(v_t.data_ptr()),
-                                          C.c_void_p(w_t.data_ptr()), op("u"), op("x"), op("f"),
-                                          op("status"), op("iters"), C.c_void_p(stream.cuda_stream)))
+                                          C.c_void_p(w_t.data_ptr()), ld_tk, ld_tb, op("u"), op("x"),
+                                          op("f"), op("fov"), op("status"), op("iters"),
+                                          C.c_void_p(stream.cuda_stream)))
 
     def set_trace(self, enable: bool):
         _lib.check(_lib.lib().nmpc_set_trace(self._h, int(enable)))

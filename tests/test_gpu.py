@@ -335,19 +335,25 @@ def test_closed_loop_kernel_matches_per_step_launches():
 
 def test_closed_loop_parity_with_oracle_loop():
     """The fused closed loop against the oracle's own solve + shift_timestep loop
-    (Python/NMPC_TT.py:348-402 restated): same statuses and applied controls."""
+    (Python/NMPC_TT.py:348-402 restated) under a target schedule that changes
+    mid-run (Python/10_obstacles.py:28-31, iterations 298..300): same statuses,
+    applied controls, states and FOV-centre errors (:397-400,433-437)."""
     import torch
     from nmpc_amd import make_spec
+    from nmpc_amd.targets import schedule
 
     spec = make_spec("race_track_2", N=10, T=0.2)
     B, K = 3, 3
-    P, bnd, vt, wt = _closed_loop_inputs(spec, B, 21)
+    P, bnd, _, _ = _closed_loop_inputs(spec, B, 21)
     f64 = dict(dtype=torch.float64, device="cuda")
+    vs, ws = schedule("10_obstacles", 298, K)
+    assert ws[1] == 0.0 and ws[2] != 0.0
+    vt, wt = torch.tensor(vs, **f64).reshape(K, 1), torch.tensor(ws, **f64).reshape(K, 1)
     s = _solver(spec)
     p = torch.tensor(P, **f64)
     w = torch.zeros(B, spec.nw, **f64)
     hist = {"u": torch.empty(K, B, 6, **f64), "x": torch.empty(K, B, 8, **f64),
-            "status": torch.empty(K, B, dtype=torch.int32, device="cuda")}
+            "fov": torch.empty(K, B, **f64), "status": torch.empty(K, B, dtype=torch.int32, device="cuda")}
     s.closed_loop_device(K, *bnd, p, w, vt, wt, hist)
     torch.cuda.synchronize()
     prob, ref = _oracle("race_track_2", 10, 0.2)
@@ -361,5 +367,8 @@ def test_closed_loop_parity_with_oracle_loop():
             if r["status"] != 0:
                 break
             assert _rel(hist["u"][k, b].cpu().numpy(), r["x"][:6]) <= TOL
-            x0, u1, xs = orc.shift_timestep(prob, x0, r["x"].reshape(spec.N, 6).T, xs)
-            u0 = u1.T.ravel()
+            x1, u1, xs1 = orc.shift_timestep(prob, x0, r["x"].reshape(spec.N, 6).T, xs, con_t=(vs[k], ws[k]))
+            xe, ye = orc.fov_centre(x1)
+            fov = np.hypot(xe - xs[0], ye - xs[1])
+            assert abs(float(hist["fov"][k, b]) - fov) <= 1e-6 * (1 + fov), (b, k)
+            x0, u0, xs = x1, u1.T.ravel(), xs1

@@ -128,3 +128,22 @@ def test_product_fails_loudly_without_gpu():
 
     with pytest.raises(_lib.NmpcError):
         nlpsol("solver", "ipopt", config_spec(3), None)
+
+
+def test_target_schedules_follow_reference_tables():
+    """con_t chains of the reference scripts' shift_timestep."""
+    import math
+    from nmpc_amd.targets import con_t, schedule, SCHEDULES
+
+    assert con_t("nmpc_tt", 0) == (12.0, 0.01)                      # NMPC_TT.py:25
+    assert con_t("10_obstacles", 299) == (13.0, 0.0)                # 10_obstacles.py:28-31
+    assert con_t("10_obstacles", 300) == (13.0, -(math.pi / 2) / 24)
+    assert con_t("10_obstacles", 2000) == (13.0, (math.pi / 2) / 12)
+    assert con_t("race_track_2", 1500) == (12.0, math.pi / 100)     # Race Track 2.py:35
+    assert con_t("plus_trajectory", 101) == (20.0, (math.pi / 2) * 5)
+    assert con_t("plus_trajectory", 102) == (20.0, 0.0)             # Plus Trajectory.py:26-29
+    assert con_t("t_trajectory", 259) == (13.5, 0.0) and con_t("t_trajectory", 260)[1] < 0
+    v, w = schedule("10_obstacles", 298, 4)
+    assert list(w[:2]) == [0.0, 0.0] and w[2] == w[3] == -(math.pi / 2) / 24 and (v == 13.0).all()
+    for name, tab in SCHEDULES.items():
+        assert [k for k, _, _ in tab] == sorted(k for k, _, _ in tab), name
