@@ -83,7 +83,7 @@ constexpr Lay make_layout(int N, int m) {
   L.sigx = g; g += al8(nw); L.ru = g; g += al8(nw);
   L.s = g; g += al8(ng); L.y = g; g += al8(ng); L.vl = g; g += al8(ng); L.vu = g; g += al8(ng);
   L.d = g; g += al8(ng); L.dt = g; g += al8(ng); L.ds = g; g += al8(ng); L.ds2 = g; g += al8(ng);
-  L.dc = g; g += al8(ng); L.dl = g; g += al8(ng); L.du = g; g += al8(ng); L.dms = g; g += al8(ng);
+  L.dc = g; g += al8(ng); L.dms = g; g += al8(ng);
   L.filt = g; g += al8(2 * FCAP + 2);
   L.gl = g; g += al8(8 * NS); L.Hl = g; g += al8(21 * NS); L.Qs = g; g += al8(36 * NS);
   L.K = g; g += al8(48 * N); L.Rk = g; g += al8(21 * N);
@@ -93,6 +93,7 @@ constexpr Lay make_layout(int N, int m) {
   L.Kc = o; o += 48; L.kf = o; o += al2(6 * N); L.Rc = o; o += 22;
   L.P0 = o; o += 64; L.P1 = o; o += 64; L.pv0 = o; o += 8; L.pv1 = o; o += 8; L.St = o; o += 48;
   L.p = o; o += 64; L.ob = o; o += al2(2 * NMPC_MAX_OBS); L.inc = o; o += al2(8 * NS); L.red = o; o += 24;
+  L.dl = o; o += al2(ng); L.du = o; o += al2(ng);  // row bounds (constant during a solve, read by every row pass)
   L.total = o;
   return L;
 }
@@ -116,20 +117,47 @@ struct IO {
   double* ws;  // per-scenario global workspace, B x wstotal
 };
 
+// Wave-wide all-reduces without LDS: DPP within 16-lane rows (quad_perm xor1,
+// xor2, row_half_mirror, row_mirror), then gfx950 permlane16/32 swaps across
+// rows.  Each step combines a lane's value with its partner's in the same
+// order on both sides, so every lane ends with a bitwise-identical result
+// (the wave-uniform decisions depend on that).
+template <int CTRL>
+__device__ __forceinline__ double dpp_d(double v) {
+  const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), CTRL, 0xF, 0xF, false);
+  return __hiloint2double(hi, lo);
+}
+struct DPair { double a, b; };
+__device__ __forceinline__ DPair swap16_d(double v) {
+  const auto lo = __builtin_amdgcn_permlane16_swap(__double2loint(v), __double2loint(v), false, false);
+  const auto hi = __builtin_amdgcn_permlane16_swap(__double2hiint(v), __double2hiint(v), false, false);
+  return {__hiloint2double(hi[0], lo[0]), __hiloint2double(hi[1], lo[1])};
+}
+__device__ __forceinline__ DPair swap32_d(double v) {
+  const auto lo = __builtin_amdgcn_permlane32_swap(__double2loint(v), __double2loint(v), false, false);
+  const auto hi = __builtin_amdgcn_permlane32_swap(__double2hiint(v), __double2hiint(v), false, false);
+  return {__hiloint2double(hi[0], lo[0]), __hiloint2double(hi[1], lo[1])};
+}
+template <class OP>
+__device__ __forceinline__ double wreduce(double v, OP op) {
+  v = op(v, dpp_d<0xB1>(v));   // quad_perm [1,0,3,2]
+  v = op(v, dpp_d<0x4E>(v));   // quad_perm [2,3,0,1]
+  v = op(v, dpp_d<0x141>(v));  // row_half_mirror
+  v = op(v, dpp_d<0x140>(v));  // row_mirror
+  const DPair p = swap16_d(v); // {row 2r, row 2r+1} in both rows of the pair
+  v = op(p.a, p.b);
+  const DPair q = swap32_d(v); // {lanes 0-31, lanes 32-63}
+  return op(q.a, q.b);
+}
 __device__ __forceinline__ double wsum(double v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, WAVE);
-  return v;
+  return wreduce(v, [](double a, double b) { return a + b; });
 }
 __device__ __forceinline__ double wmax(double v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, WAVE));
-  return v;
+  return wreduce(v, [](double a, double b) { return fmax(a, b); });
 }
 __device__ __forceinline__ double wmin(double v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = fmin(v, __shfl_xor(v, o, WAVE));
-  return v;
+  return wreduce(v, [](double a, double b) { return fmin(a, b); });
 }
 __device__ __forceinline__ bool wany(bool b) { return __any((int)b) != 0; }
 __device__ __forceinline__ double readlane_d(double v, int l) {
@@ -155,7 +183,16 @@ __device__ __forceinline__ double rsq(double x) {
   r = fma(-h * y, y, 0.5);
   return fma(y, r, y);
 }
-__device__ __forceinline__ void sync() { __syncthreads(); }
+// Cross-lane hand-off inside the (single-wave) workgroup.  Every kernel here runs
+// exactly one wavefront per workgroup, so a wavefront-scope fence is the complete
+// synchronisation: it orders the compiler's memory operations (LDS and global)
+// and, per the AMDGPU memory model, needs no hardware wait because a wave's memory
+// operations are performed in order.  (__syncthreads' workgroup-scope release
+// would wait for every outstanding global store, s_waitcnt vmcnt(0), each time.)
+__device__ __forceinline__ void sync() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
 
 // packed index of the symmetric 6x6 local (x,y,z,x5,x6,x7) Hessian, a <= b
 __device__ __forceinline__ int hp(int a, int b) {
@@ -189,6 +226,10 @@ enum Phase { PH_ROLLOUT, PH_EVAL, PH_DERIVS, PH_ADJ, PH_SUMM, PH_RIC, PH_RESOLVE
 
 template <class CAP>
 struct Solver {
+  // stage loops with a lane-dependent range run to the class maximum with a guard
+  // (fully unrolled, so their loads issue together) for classes up to 32 stages
+  static constexpr bool kUnrollStages = CAP::nmax <= 32;
+  static constexpr int kStageUnroll = kUnrollStages ? CAP::nmax : 1;
   const CST Params* __restrict__ P;
   LDS double* sm;
   int lane_, b;
@@ -201,7 +242,8 @@ struct Solver {
   // pointers into LDS
   GLB double* U, *Ut, *dU, *dU2, *zl, *zu, *xl, *xu, *sigx, *ru;
   LDS double* X, *Xt, *dX;
-  GLB double* s, *y, *vl, *vu, *d, *dt, *ds, *ds2, *dc, *dl, *du, *dms;
+  GLB double* s, *y, *vl, *vu, *d, *dt, *ds, *ds2, *dc, *dms;
+  LDS double *dl, *du;
   GLB double* gl, *Hl, *Qs;
   LDS double* trig, *qs, *lam;
   GLB double* K, *Rk;
@@ -224,7 +266,7 @@ struct Solver {
     X = sm + L.X; Xt = sm + L.Xt; dX = sm + L.dX;
     s = gw + L.s; y = gw + L.y; vl = gw + L.vl; vu = gw + L.vu;
     d = gw + L.d; dt = gw + L.dt; ds = gw + L.ds; ds2 = gw + L.ds2;
-    dc = gw + L.dc; dl = gw + L.dl; du = gw + L.du; dms = gw + L.dms;
+    dc = gw + L.dc; dl = sm + L.dl; du = sm + L.du; dms = gw + L.dms;
     gl = gw + L.gl; Hl = gw + L.Hl; trig = sm + L.trig; Qs = gw + L.Qs; qs = sm + L.qs;
     lam = sm + L.lam;
     K = gw + L.K; kf = sm + L.kf; Rk = gw + L.Rk; Kc = sm + L.Kc; Rc = sm + L.Rc;
@@ -254,9 +296,13 @@ struct Solver {
     if (k <= N) {
 #pragma unroll
       for (int c = 0; c < 5; ++c) a[c] = pp[3 + c];
-      for (int j = 0; j < k; ++j) {
+      const int jlim = kUnrollStages ? CAP::nmax : k;
+#pragma unroll kStageUnroll
+      for (int j = 0; j < jlim; ++j) {
+        if (j < k) {
 #pragma unroll
-        for (int c = 0; c < 5; ++c) a[c] = a[c] + inc[j * 8 + c];
+          for (int c = 0; c < 5; ++c) a[c] = a[c] + inc[j * 8 + c];
+        }
       }
       if (k < N) {
         const double v = Us[k * 6];
@@ -269,10 +315,14 @@ struct Solver {
     sync();
     if (k <= N) {
       double c0 = pp[0], c1 = pp[1], c2 = pp[2];
-      for (int j = 0; j < k; ++j) {
-        c0 = c0 + inc[j * 8 + 5];
-        c1 = c1 + inc[j * 8 + 6];
-        c2 = c2 + inc[j * 8 + 7];
+      const int jlim = kUnrollStages ? CAP::nmax : k;
+#pragma unroll kStageUnroll
+      for (int j = 0; j < jlim; ++j) {
+        if (j < k) {
+          c0 = c0 + inc[j * 8 + 5];
+          c1 = c1 + inc[j * 8 + 6];
+          c2 = c2 + inc[j * 8 + 7];
+        }
       }
       LDS double* xk = Xd + k * 8;
       xk[0] = c0; xk[1] = c1; xk[2] = c2;
@@ -456,13 +506,21 @@ struct Solver {
           const int r = k * m + i;
           w[boxidx(i)] += dc[r] * yy[r];
         }
-        for (int o = 0; o < nobs; ++o) {
+        // compile-time bound so every row's loads issue before the first use
+        double cyv[CAP::mmax - 5];
+#pragma unroll
+        for (int o = 0; o < CAP::mmax - 5; ++o) {
           const int r = k * m + 5 + o;
-          const double ddx = xk[0] - obx[o], ddy = xk[1] - oby[o];
-          const double idd = rsq(ddx * ddx + ddy * ddy);
-          const double cy = dc[r] * yy[r];
-          w[0] += cy * (-(ddx * idd));
-          w[1] += cy * (-(ddy * idd));
+          cyv[o] = o < nobs ? dc[r] * yy[r] : 0.0;
+        }
+#pragma unroll
+        for (int o = 0; o < CAP::mmax - 5; ++o) {
+          if (o < nobs) {
+            const double ddx = xk[0] - obx[o], ddy = xk[1] - oby[o];
+            const double idd = rsq(ddx * ddx + ddy * ddy);
+            w[0] += cyv[o] * (-(ddx * idd));
+            w[1] += cyv[o] * (-(ddy * idd));
+          }
         }
       }
 #pragma unroll
@@ -471,23 +529,33 @@ struct Solver {
     sync();
     if (k <= N) {
       const int cs[6] = {0, 1, 2, 5, 6, 7};
+      double acc[6];
 #pragma unroll
-      for (int q = 0; q < 6; ++q) {
-        const int c = cs[q];
-        double acc = wv[N * 8 + c];
-        for (int j = N - 1; j >= k; --j) acc = wv[j * 8 + c] + acc;
-        lam[k * 8 + c] = acc;
+      for (int q = 0; q < 6; ++q) acc[q] = wv[N * 8 + cs[q]];
+      // suffix sums in the oracle's order (j = N-1 down to k), unrolled to the
+      // class maximum so the LDS reads pipeline
+#pragma unroll kStageUnroll
+      for (int jj = (kUnrollStages ? CAP::nmax : N) - 1; jj >= 0; --jj) {
+        if (jj < N && jj >= k) {
+#pragma unroll
+          for (int q = 0; q < 6; ++q) acc[q] = wv[jj * 8 + cs[q]] + acc[q];
+        }
       }
+#pragma unroll
+      for (int q = 0; q < 6; ++q) lam[k * 8 + cs[q]] = acc[q];
     }
     sync();
     if (k <= N) {
       double a3 = wv[N * 8 + 3], a4 = wv[N * 8 + 4];
-      for (int j = N - 1; j >= k; --j) {
-        double E03, E04, E13, E14, E23, b00, b10, b20;
-        stage_AB(j, E03, E04, E13, E14, E23, b00, b10, b20);
-        const LDS double* ln = lam + (j + 1) * 8;
-        a3 = wv[j * 8 + 3] + (((E03 * ln[0] + E13 * ln[1]) + E23 * ln[2]) + a3);
-        a4 = wv[j * 8 + 4] + ((E04 * ln[0] + E14 * ln[1]) + a4);
+#pragma unroll kStageUnroll
+      for (int j = (kUnrollStages ? CAP::nmax : N) - 1; j >= 0; --j) {
+        if (j < N && j >= k) {
+          double E03, E04, E13, E14, E23, b00, b10, b20;
+          stage_AB(j, E03, E04, E13, E14, E23, b00, b10, b20);
+          const LDS double* ln = lam + (j + 1) * 8;
+          a3 = wv[j * 8 + 3] + (((E03 * ln[0] + E13 * ln[1]) + E23 * ln[2]) + a3);
+          a4 = wv[j * 8 + 4] + ((E04 * ln[0] + E14 * ln[1]) + a4);
+        }
       }
       lam[k * 8 + 3] = a3;
       lam[k * 8 + 4] = a4;
@@ -870,12 +938,24 @@ struct Solver {
     for (int i = 0; i < 8; ++i) dx[i] = 0.0;
     if (lanef() < 8) dXo[lanef()] = 0.0;
     const int r = lanef() < 6 ? lanef() : 5;
+    // K_k rows come from global memory and do not depend on dx: fetch stage k+1's
+    // row while stage k is being formed
+    double Kn[8];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) Kn[c] = K[r * 8 + c];
     for (int k = 0; k < N; ++k) {
+      double Kr[8];
+#pragma unroll
+      for (int c = 0; c < 8; ++c) Kr[c] = Kn[c];
+      if (k + 1 < N) {
+#pragma unroll
+        for (int c = 0; c < 8; ++c) Kn[c] = K[(k + 1) * 48 + r * 8 + c];
+      }
       double E03, E04, E13, E14, E23, b00, b10, b20;
       stage_AB(k, E03, E04, E13, E14, E23, b00, b10, b20);
       double a = kf[k * 6 + r];
 #pragma unroll
-      for (int c = 0; c < 8; ++c) a += K[k * 48 + r * 8 + c] * dx[c];
+      for (int c = 0; c < 8; ++c) a += Kr[c] * dx[c];
       if (lanef() < 6) dUo[k * 6 + lanef()] = a;
       double du_[6];
 #pragma unroll
@@ -915,6 +995,41 @@ struct Solver {
       }
       const double rd = rd_is_dms ? rdsrc[r] : d[r] - s[r];
       dso[r] = jd + rd;
+    }
+    STAMP1(PH_ROWSTEP);
+    sync();
+  }
+
+  // Newton-direction row step fused with the line-search set-up sums over the
+  // same rows: theta = sum |d - s|, the slack part of grad(phi)^T d, and the
+  // tiny-step ratio max |ds| / (1 + |s|) (per-lane partials; caller reduces)
+  __device__ __forceinline__ void row_step_ls(const LDS double* dXs, double mu_, double& th, double& g, double& msv) {
+    STAMP0();
+    const double kd = P->o.kappa_d;
+    th = 0.0; g = 0.0; msv = 0.0;
+    for (int r = lanef(); r < ng; r += WAVE) {
+      const int k = r / m, i = r - k * m;
+      const LDS double* xk = X + k * 8;
+      const LDS double* dxk = dXs + k * 8;
+      double jd;
+      if (i < 5) {
+        jd = dc[r] * dxk[boxidx(i)];
+      } else {
+        const int o = i - 5;
+        const double ddx = xk[0] - obx[o], ddy = xk[1] - oby[o];
+        const double idd = rsq(ddx * ddx + ddy * ddy);
+        jd = dc[r] * ((-(ddx * idd)) * dxk[0] + (-(ddy * idd)) * dxk[1]);
+      }
+      const double sr = s[r], dr = d[r];
+      const double dsr = jd + (dr - sr);
+      ds[r] = dsr;
+      th += fabs(dr - sr);
+      const double lo = dl[r], hi = du[r];
+      const bool hl = hasl(lo), hu = hasu(hi);
+      const double gs = -(hl ? mu_ / (sr - lo) : 0.0) + (hu ? mu_ / (hi - sr) : 0.0) +
+                        kd * mu_ * ((hl && !hu ? 1.0 : 0.0) - (hu && !hl ? 1.0 : 0.0));
+      g += gs * dsr;
+      msv = fmax(msv, fabs(dsr / (1.0 + fabs(sr))));
     }
     STAMP1(PH_ROWSTEP);
     sync();
@@ -1002,25 +1117,41 @@ struct Solver {
     return !wany(!ok);
   }
   __device__ __forceinline__ void filter_add(double phi, double th) {
-    // drop entries dominated by the new one, then append (IpFilter::AddEntry)
-    sync();
-    if (lanef() == 0) {
-      int w = 0;
-      for (int e = 0; e < nfilt; ++e) {
-        const double fp = filt[2 * e], ft = filt[2 * e + 1];
-        if (!(fp >= phi && ft >= th)) {
-          filt[2 * w] = fp; filt[2 * w + 1] = ft; ++w;
-        }
-      }
-      if (w >= FCAP) {  // capacity guard: drop the oldest entry
-        for (int e = 1; e < w; ++e) { filt[2 * e - 2] = filt[2 * e]; filt[2 * e - 1] = filt[2 * e + 1]; }
-        --w;
-      }
-      filt[2 * w] = phi; filt[2 * w + 1] = th;
-      filt[2 * FCAP] = (double)(w + 1);
+    // drop entries dominated by the new one, then append (IpFilter::AddEntry);
+    // lane-parallel: every lane reads its entries, kept ones are compacted with
+    // ballot + mbcnt, so the update costs one global round trip, not nfilt
+    constexpr int FCH = (FCAP + WAVE - 1) / WAVE;
+    double fp[FCH], ft[FCH];
+    bool keep[FCH];
+#pragma unroll
+    for (int c = 0; c < FCH; ++c) {
+      const int e = lanef() + c * WAVE;
+      const bool valid = e < nfilt;
+      fp[c] = valid ? filt[2 * e] : 0.0;
+      ft[c] = valid ? filt[2 * e + 1] : 0.0;
+      keep[c] = valid && !(fp[c] >= phi && ft[c] >= th);
     }
     sync();
-    nfilt = (int)filt[2 * FCAP];
+    int w = 0;
+#pragma unroll
+    for (int c = 0; c < FCH; ++c) {
+      const unsigned long long mask = __ballot(keep[c]);
+      const int pos = w + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(mask >> 32),
+                                                         __builtin_amdgcn_mbcnt_lo((unsigned)mask, 0u));
+      if (keep[c]) { filt[2 * pos] = fp[c]; filt[2 * pos + 1] = ft[c]; }
+      w += __popcll(mask);
+    }
+    sync();
+    if (w >= FCAP) {  // capacity guard: drop the oldest entry (never reached with max_iter <= FCAP)
+      if (lanef() == 0) {
+        for (int e = 1; e < w; ++e) { filt[2 * e - 2] = filt[2 * e]; filt[2 * e - 1] = filt[2 * e + 1]; }
+      }
+      --w;
+      sync();
+    }
+    if (lanef() == 0) { filt[2 * w] = phi; filt[2 * w + 1] = th; }
+    sync();
+    nfilt = w + 1;
   }
 
   // trial point u = U + a dUs, s = s + a dss: rollout into Xt, rows into dt.
@@ -1370,20 +1501,17 @@ __device__ __forceinline__ void solve_one(Solver<CAP>& S, const Params* __restri
     S.delta = delta;
     if (!fact_ok) { status = ST_STEP_ERR; break; }
     S.forward(S.dU, S.dX);
-    S.row_step(S.dX, nullptr, false, S.ds);
 
     // ===== line search (BacktrackingLineSearch + FilterLSAcceptor)
-    double theta_ref = 0.0, gbd = 0.0;
+    double theta_ref = 0.0, gbd = 0.0, tiny_mx = 0.0, tiny_msv = 0.0;
     {
-      double th = 0.0, g = 0.0;
-      for (int r = S.lanef(); r < ng; r += WAVE) {
-        th += fabs(S.d[r] - S.s[r]);
-        const bool hl = S.hasl(S.dl[r]), hu = S.hasu(S.du[r]);
-        const double gs = -(hl ? mu / (S.s[r] - S.dl[r]) : 0.0) + (hu ? mu / (S.du[r] - S.s[r]) : 0.0) +
-                          o.kappa_d * mu * ((hl && !hu ? 1.0 : 0.0) - (hu && !hl ? 1.0 : 0.0));
-        g += gs * S.ds[r];
+      double th, g, msv, mx = 0.0;
+      S.row_step_ls(S.dX, mu, th, g, msv);
+      for (int i = S.lanef(); i < nw; i += WAVE) {
+        const double du_ = S.dU[i];
+        g += S.ru[i] * du_;
+        mx = fmax(mx, fabs(du_ / (1.0 + fabs(S.U[i]))));
       }
-      for (int i = S.lanef(); i < nw; i += WAVE) g += S.ru[i] * S.dU[i];
       if (S.lanef() <= N) {
         double gx = 0.0;
 #pragma unroll
@@ -1392,6 +1520,8 @@ __device__ __forceinline__ void solve_one(Solver<CAP>& S, const Params* __restri
       }
       theta_ref = wsum(th);
       gbd = wsum(g);
+      tiny_mx = wmax(mx);
+      tiny_msv = wmax(msv);
     }
     const double phi_ref = S.barrier_obj(f, S.U, S.s, nullptr, 0.0);
     if (theta_max < 0) {
@@ -1503,12 +1633,8 @@ __device__ __forceinline__ void solve_one(Solver<CAP>& S, const Params* __restri
         if (r == 2) in_soft = false;
       }
     } else {
-      // tiny step detection (BacktrackingLineSearch::DetectTinyStep)
-      double mx = 0.0, msv = 0.0;
-      for (int i = S.lanef(); i < nw; i += WAVE) mx = fmax(mx, fabs(S.dU[i] / (1.0 + fabs(S.U[i]))));
-      for (int r = S.lanef(); r < ng; r += WAVE) msv = fmax(msv, fabs(S.ds[r] / (1.0 + fabs(S.s[r]))));
-      mx = wmax(mx); msv = wmax(msv);
-      const bool tiny = mx <= o.tiny_step_tol && msv <= o.tiny_step_tol && pinf <= 1e-4;
+      // tiny step detection (BacktrackingLineSearch::DetectTinyStep; ratios from row_step_ls)
+      const bool tiny = tiny_mx <= o.tiny_step_tol && tiny_msv <= o.tiny_step_tol && pinf <= 1e-4;
       if (tiny) {
         const double a = S.frac_to_bound(tau, S.dU, S.ds);
         double ft, phit, tht;
@@ -1711,17 +1837,16 @@ __global__ __launch_bounds__(WAVE, NMPC_WAVES_PER_EU) void nmpc_closed_loop_kern
   extern __shared__ __attribute__((aligned(16))) double smem[];
   const int b = blockIdx.x;
   if (b >= B) return;
-  Solver<CAP> S;
-  S.bind(prm, smem, io.ws, threadIdx.x, b);
-  const int nw = S.nw, N = S.N;
-  const double T = S.T;
+  const int nw = prm->nw;
+  const double T = prm->T;
   double* wb = lp.w + (long long)b * nw;
   double* pb = lp.p + (long long)b * lp.ld_p;
   constexpr int WR = (6 * CAP::nmax + WAVE - 1) / WAVE;
   for (int k = 0; k < lp.K; ++k) {
-    // re-derive every per-lane address each step from an opaque lane index, so the
-    // compiler keeps nothing live across steps (hoisting them costs ~40 VGPRs of spills)
-    S.bind(prm, smem, io.ws, S.lanef(), b);
+    // a fresh solver per step: no member is live across steps (a solver kept
+    // outside the loop costs ~40 VGPRs of spills)
+    Solver<CAP> S;
+    S.bind(prm, smem, io.ws, threadIdx.x, b);
     IO ik = io;
     ik.x0 = lp.w; ik.ld_x0 = nw; ik.x_out = lp.w;
     ik.p = lp.p; ik.ld_p = lp.ld_p;
@@ -1774,7 +1899,6 @@ __global__ __launch_bounds__(WAVE, NMPC_WAVES_PER_EU) void nmpc_closed_loop_kern
       const int i = l + j * WAVE;
       if (i < nw) wb[i] = wn[j];
     }
-    (void)N;
     sync();
   }
 }
