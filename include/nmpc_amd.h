@@ -30,7 +30,8 @@
  * Non-convergence is NOT an error (the reference never checks it):
  * it is reported per scenario in status[] with IPOPT's ApplicationReturnStatus
  * codes (Ipopt::Solve_Succeeded = 0, Solved_To_Acceptable_Level = 1,
- * Search_Direction_Becomes_Too_Small = 3, Maximum_Iterations_Exceeded = -1,
+ * Infeasible_Problem_Detected = 2, Search_Direction_Becomes_Too_Small = 3,
+ * Maximum_Iterations_Exceeded = -1,
  * Restoration_Failed = -2, Error_In_Step_Computation = -3,
  * Invalid_Number_Detected = -13).
  *
@@ -77,6 +78,9 @@ typedef struct nmpc_options {
   double first_hessian_perturbation, min_hessian_perturbation, max_hessian_perturbation;
   double perturb_inc_fact_first, perturb_inc_fact, perturb_dec_fact;
   double tiny_step_tol, soft_resto_pderror_reduction_factor;
+  /* feasibility restoration phase */
+  double resto_penalty_parameter, resto_proximity_weight, required_infeasibility_reduction;
+  double bound_mult_reset_threshold, constr_mult_reset_threshold;
 } nmpc_options;
 
 /* Structured replacement for the symbolic nlp_prob of Python/NMPC_TT.py:247-255. */

@@ -44,7 +44,7 @@ constexpr int FCAP = 128;      // filter capacity (>= max_iter of the reference 
 constexpr int TRACE_F = NMPC_TRACE_FIELDS;
 
 // ---- status codes (IPOPT ApplicationReturnStatus) ----
-constexpr int ST_SUCCESS = 0, ST_ACCEPTABLE = 1, ST_TINY = 3, ST_MAXITER = -1,
+constexpr int ST_SUCCESS = 0, ST_ACCEPTABLE = 1, ST_INFEASIBLE = 2, ST_TINY = 3, ST_MAXITER = -1,
               ST_RESTO_FAIL = -2, ST_STEP_ERR = -3, ST_INVALID_PROBLEM = -11,
               ST_INVALID_NUMBER = -13;
 
@@ -64,11 +64,14 @@ struct Lay {
   int U, Ut, dU, dU2, zl, zu, xl, xu, sigx, ru;
   int s, y, vl, vu, d, dt, ds, ds2, dc, dl, du, dms, filt;
   int gl, Hl, Qs, K, Rk;        // stage data / Riccati factors (global copies)
+  // restoration phase: reference/backup iterate, p/n and their multipliers, steps, filter
+  int UR, zl0, zu0, s0, vl0, vu0, pR, nR, zpR, znR, dpR, dnR, dyR, dp2R, dn2R, dy2R, cms, filtR;
+  int accU, accZl, accZu, accY;  // last acceptable iterate (BacktrackingLineSearch::StoreAcceptablePoint)
   // LDS
   int X, Xt, dX;
   int trig, qs, lam;
   int Kc, kf, Rc, P0, P1, pv0, pv1, St;
-  int p, ob, inc, red;
+  int p, ob, inc, red, rvars;
   int total;    // LDS doubles per scenario
   int wstotal;  // global-workspace doubles per scenario
 };
@@ -87,6 +90,13 @@ constexpr Lay make_layout(int N, int m) {
   L.filt = g; g += al8(2 * FCAP + 2);
   L.gl = g; g += al8(8 * NS); L.Hl = g; g += al8(21 * NS); L.Qs = g; g += al8(36 * NS);
   L.K = g; g += al8(48 * N); L.Rk = g; g += al8(21 * N);
+  L.UR = g; g += al8(nw); L.zl0 = g; g += al8(nw); L.zu0 = g; g += al8(nw);
+  L.s0 = g; g += al8(ng); L.vl0 = g; g += al8(ng); L.vu0 = g; g += al8(ng);
+  L.pR = g; g += al8(ng); L.nR = g; g += al8(ng); L.zpR = g; g += al8(ng); L.znR = g; g += al8(ng);
+  L.dpR = g; g += al8(ng); L.dnR = g; g += al8(ng); L.dyR = g; g += al8(ng);
+  L.dp2R = g; g += al8(ng); L.dn2R = g; g += al8(ng); L.dy2R = g; g += al8(ng); L.cms = g; g += al8(ng);
+  L.filtR = g; g += al8(2 * FCAP + 2);
+  L.accU = g; g += al8(nw); L.accZl = g; g += al8(nw); L.accZu = g; g += al8(nw); L.accY = g; g += al8(ng);
   L.wstotal = g;
   L.X = o; o += al2(nX); L.Xt = o; o += al2(nX); L.dX = o; o += al2(nX);
   L.trig = o; o += al2(8 * NS); L.qs = o; o += al2(10 * NS); L.lam = o; o += al2(8 * NS);
@@ -94,6 +104,7 @@ constexpr Lay make_layout(int N, int m) {
   L.P0 = o; o += 64; L.P1 = o; o += 64; L.pv0 = o; o += 8; L.pv1 = o; o += 8; L.St = o; o += 48;
   L.p = o; o += 64; L.ob = o; o += al2(2 * NMPC_MAX_OBS); L.inc = o; o += al2(8 * NS); L.red = o; o += 24;
   L.dl = o; o += al2(ng); L.du = o; o += al2(ng);  // row bounds (constant during a solve, read by every row pass)
+  L.rvars = o; o += 32;  // restoration-phase scalars
   L.total = o;
   return L;
 }
@@ -207,7 +218,7 @@ __device__ __forceinline__ int boxidx(int i) {  // g rows 0..4: z, theta, x5, x6
   return i == 0 ? 2 : (i == 1 ? 3 : 3 + i);
 }
 
-enum SumMode { SUM_NEWTON = 0, SUM_LS = 1, SUM_SOC = 2 };
+enum SumMode { SUM_NEWTON = 0, SUM_LS = 1, SUM_SOC = 2, SUM_RESTO = 3, SUM_RESTO_SOC = 4, SUM_LS_RESTO = 5 };
 
 // Diagnostic phase timers (-DNMPC_STAMPS builds only): shader-clock cycles per
 // phase, accumulated by lane 0 in LDS and written to the two spare rows of the
@@ -243,7 +254,11 @@ struct Solver {
   GLB double* U, *Ut, *dU, *dU2, *zl, *zu, *xl, *xu, *sigx, *ru;
   LDS double* X, *Xt, *dX;
   GLB double* s, *y, *vl, *vu, *d, *dt, *ds, *ds2, *dc, *dms;
-  LDS double *dl, *du;
+  GLB double *UR, *zl0, *zu0, *s0, *vl0, *vu0, *pR, *nR, *zpR, *znR, *dpR, *dnR, *dyR, *dp2R, *dn2R, *dy2R, *cms, *filtR;
+  GLB double *accU, *accZl, *accZu, *accY;
+  double rho, etaR;  // restoration: penalty, proximity weight * sqrt(mu)
+  double* wsbase;    // workspace base of all scenarios (restoration re-binds from it)
+  LDS double *dl, *du, *rvars;
   GLB double* gl, *Hl, *Qs;
   LDS double* trig, *qs, *lam;
   GLB double* K, *Rk;
@@ -259,6 +274,7 @@ struct Solver {
     constexpr Lay L = CAP::L;
     P = (const CST Params*)prm; sm = (LDS double*)smem; this->lane_ = lane_; b = b_;
     N = prm->N; m = prm->m; nobs = prm->nobs; nw = prm->nw; ng = prm->ng; T = prm->T;
+    wsbase = wsp;
     GLB double* gw = (GLB double*)(wsp + (long long)b_ * L.wstotal);
     U = gw + L.U; Ut = gw + L.Ut; dU = gw + L.dU; dU2 = gw + L.dU2;
     zl = gw + L.zl; zu = gw + L.zu; xl = gw + L.xl; xu = gw + L.xu;
@@ -266,7 +282,12 @@ struct Solver {
     X = sm + L.X; Xt = sm + L.Xt; dX = sm + L.dX;
     s = gw + L.s; y = gw + L.y; vl = gw + L.vl; vu = gw + L.vu;
     d = gw + L.d; dt = gw + L.dt; ds = gw + L.ds; ds2 = gw + L.ds2;
-    dc = gw + L.dc; dl = sm + L.dl; du = sm + L.du; dms = gw + L.dms;
+    dc = gw + L.dc; dl = sm + L.dl; du = sm + L.du; dms = gw + L.dms; rvars = sm + L.rvars;
+    UR = gw + L.UR; zl0 = gw + L.zl0; zu0 = gw + L.zu0; s0 = gw + L.s0; vl0 = gw + L.vl0; vu0 = gw + L.vu0;
+    pR = gw + L.pR; nR = gw + L.nR; zpR = gw + L.zpR; znR = gw + L.znR; dpR = gw + L.dpR; dnR = gw + L.dnR;
+    dyR = gw + L.dyR; dp2R = gw + L.dp2R; dn2R = gw + L.dn2R; dy2R = gw + L.dy2R; cms = gw + L.cms;
+    filtR = gw + L.filtR;
+    accU = gw + L.accU; accZl = gw + L.accZl; accZu = gw + L.accZu; accY = gw + L.accY;
     gl = gw + L.gl; Hl = gw + L.Hl; trig = sm + L.trig; Qs = gw + L.Qs; qs = sm + L.qs;
     lam = sm + L.lam;
     K = gw + L.K; kf = sm + L.kf; Rk = gw + L.Rk; Kc = sm + L.Kc; Rc = sm + L.Rc;
@@ -628,6 +649,17 @@ struct Solver {
         if (mode == SUM_LS) {
           A = 1.0;
           Bw = -(vu[r] - vl[r]);
+        } else if (mode == SUM_LS_RESTO) {
+          // (I + J^T J / 3) w = bx + J^T (bs + bp - bn) / 3 : the restoration NLP's
+          // least-squares multipliers with p, n eliminated
+          A = 1.0 / 3.0;
+          Bw = -((vu[r] - vl[r]) + (rho - zpR[r]) - (rho - znR[r])) / 3.0;
+        } else if (mode == SUM_RESTO || mode == SUM_RESTO_SOC) {
+          double D, rs, Sp, Sn, rp, rn, Dt, Dr;
+          row_resto(r, mode == SUM_RESTO_SOC, D, rs, Sp, Sn, rp, rn, Dt, Dr);
+          A = Dt;
+          Bw = y[r] + Dr;
+          C = y[r] * dc[r];
         } else {
           const bool lo = hasl(dl[r]), hi = hasu(du[r]);
           const double iSl = lo ? rcp(s[r] - dl[r]) : 0.0, iSu = hi ? rcp(du[r] - s[r]) : 0.0;
@@ -665,7 +697,7 @@ struct Solver {
       qo[5] = gfac * gl[k * 8 + 5] + qb[2];
       qo[6] = gfac * gl[k * 8 + 6] + qb[3];
       qo[7] = gfac * gl[k * 8 + 7] + qb[4];
-      if (mode != SUM_SOC) {
+      if (mode != SUM_SOC && mode != SUM_RESTO_SOC) {
         double Q[36];
 #pragma unroll
         for (int t = 0; t < 36; ++t) Q[t] = 0.0;
@@ -1035,6 +1067,127 @@ struct Solver {
     sync();
   }
 
+  // ------------------------------------------------ restoration phase rows
+  // p, n (d(x) - s - p + n = 0, p, n >= 0) eliminated per row: weight
+  // D~ = (1/D + 1/Sp + 1/Sn)^-1 and right-hand side D~ r~ (oracle restoration()),
+  // written without 1/D so rows with no bound (D = 0) stay finite.
+  __device__ __forceinline__ void row_resto(int r, bool soc, double& D, double& rs, double& Sp, double& Sn,
+                                            double& rp, double& rn, double& Dt, double& Dr) const {
+    row_rs(r, D, rs);
+    const double kd = P->o.kappa_d;
+    const double pr = pR[r], nr = nR[r];
+    const double ip = 1.0 / pr, in_ = 1.0 / nr;
+    Sp = zpR[r] * ip + delta;
+    Sn = znR[r] * in_ + delta;
+    rp = rho - y[r] - mu * ip + kd * mu;
+    rn = rho + y[r] - mu * in_ + kd * mu;
+    const double c = soc ? cms[r] : d[r] - s[r] - pr + nr;
+    const double iSp = 1.0 / Sp, iSn = 1.0 / Sn;
+    const double den = 1.0 / (1.0 + D * (iSp + iSn));
+    Dt = D * den;
+    Dr = Dt * (c + rp * iSp - rn * iSn) + rs * den;
+  }
+  __device__ __forceinline__ double dr2(int i) const {  // D_R^2 = 1/max(1,|x_R|)^2
+    const double a = fmax(1.0, fabs(UR[i]));
+    return 1.0 / (a * a);
+  }
+  // restoration step rows: dy, dp, dn, ds (= J dx + c - dp + dn); for the Newton
+  // direction also theta_R and the slack/p/n part of grad(phi_R)^T d
+  __device__ __forceinline__ void row_step_resto(const LDS double* dXs, bool soc, GLB double* dso, GLB double* dpo,
+                                                 GLB double* dno, GLB double* dyo, double& th, double& gsum) {
+    const double kd = P->o.kappa_d;
+    th = 0.0; gsum = 0.0;
+    for (int r = lanef(); r < ng; r += WAVE) {
+      const int k = r / m, i = r - k * m;
+      const LDS double* xk = X + k * 8;
+      const LDS double* dxk = dXs + k * 8;
+      double jd;
+      if (i < 5) {
+        jd = dc[r] * dxk[boxidx(i)];
+      } else {
+        const int o = i - 5;
+        const double ddx = xk[0] - obx[o], ddy = xk[1] - oby[o];
+        const double idd = rsq(ddx * ddx + ddy * ddy);
+        jd = dc[r] * ((-(ddx * idd)) * dxk[0] + (-(ddy * idd)) * dxk[1]);
+      }
+      double D, rs, Sp, Sn, rp, rn, Dt, Dr;
+      row_resto(r, soc, D, rs, Sp, Sn, rp, rn, Dt, Dr);
+      const double c = soc ? cms[r] : d[r] - s[r] - pR[r] + nR[r];
+      const double dyv = Dt * jd + Dr;
+      const double dpv = (dyv - rp) / Sp, dnv = (-dyv - rn) / Sn;
+      const double dsv = jd + c - dpv + dnv;
+      dso[r] = dsv; dpo[r] = dpv; dno[r] = dnv; dyo[r] = dyv;
+      if (!soc) {
+        th += fabs(c);
+        const double lo = dl[r], hi = du[r], sr = s[r];
+        const bool hl = hasl(lo), hu = hasu(hi);
+        const double gs = -(hl ? mu / (sr - lo) : 0.0) + (hu ? mu / (hi - sr) : 0.0) +
+                          kd * mu * ((hl && !hu ? 1.0 : 0.0) - (hu && !hl ? 1.0 : 0.0));
+        gsum += gs * dsv + (rho - mu / pR[r] + kd * mu) * dpv + (rho - mu / nR[r] + kd * mu) * dnv;
+      }
+    }
+    sync();
+  }
+  // p, n part of phi_R at s + a ds, p + a dp, n + a dn (the x/s part comes from barrier_obj)
+  __device__ __forceinline__ double resto_pn_terms(const GLB double* Us, double a, const GLB double* dps,
+                                                   const GLB double* dns) const {
+    double pn = 0.0, lg = 0.0, prox = 0.0;
+    for (int r = lanef(); r < ng; r += WAVE) {
+      const double pv = dps ? pR[r] + a * dps[r] : pR[r], nv = dns ? nR[r] + a * dns[r] : nR[r];
+      pn += pv + nv;
+      lg += log(pv) + log(nv);
+    }
+    for (int i = lanef(); i < nw; i += WAVE) {
+      const double dd = Us[i] - UR[i];
+      prox += dr2(i) * dd * dd;
+    }
+    pn = wsum(pn); lg = wsum(lg); prox = wsum(prox);
+    return rho * pn + 0.5 * etaR * prox - mu * lg + P->o.kappa_d * mu * pn;
+  }
+  // restoration trial point: theta_R, phi_R and the original objective fo
+  __device__ __forceinline__ bool trial_resto(double a, const GLB double* dUs, const GLB double* dss,
+                                              const GLB double* dps, const GLB double* dns, double& fo,
+                                              double& phit, double& tht) {
+    for (int i = lanef(); i < nw; i += WAVE) Ut[i] = U[i] + a * dUs[i];
+    sync();
+    rollout(Ut, Xt);
+    fo = df * eval_fg(Xt, dt, dc);
+    double th = 0.0;
+    bool bad = false;
+    for (int r = lanef(); r < ng; r += WAVE) {
+      const double sv = s[r] + a * dss[r], pv = pR[r] + a * dps[r], nv = nR[r] + a * dns[r];
+      th += fabs(dt[r] - sv - pv + nv);
+      if (!isfinite(dt[r])) bad = true;
+    }
+    tht = wsum(th);
+    if (wany(bad)) return false;
+    phit = barrier_obj(0.0, Ut, s, dss, a) + resto_pn_terms(Ut, a, dps, dns);
+    return isfinite(phit);
+  }
+  __device__ __forceinline__ double frac_to_bound_resto(double tau_, const GLB double* dUs, const GLB double* dss,
+                                                        const GLB double* dps, const GLB double* dns) const {
+    double a = frac_to_bound(tau_, dUs, dss);
+    double b = 1.0;
+    for (int r = lanef(); r < ng; r += WAVE) {
+      if (dps[r] < 0) b = fmin(b, (-tau_ * pR[r]) / dps[r]);
+      if (dns[r] < 0) b = fmin(b, (-tau_ * nR[r]) / dns[r]);
+    }
+    return fmin(a, wmin(b));
+  }
+  __device__ __forceinline__ double dual_frac_to_bound_resto(double tau_, const GLB double* dUs, const GLB double* dss,
+                                                             const GLB double* dps, const GLB double* dns) const {
+    double a = dual_frac_to_bound(tau_, dUs, dss);
+    double b = 1.0;
+    for (int r = lanef(); r < ng; r += WAVE) {
+      const double pr = pR[r], nr = nR[r];
+      const double dzp = mu / pr - zpR[r] - (zpR[r] / pr) * dps[r];
+      const double dzn = mu / nr - znR[r] - (znR[r] / nr) * dns[r];
+      if (dzp < 0) b = fmin(b, (-tau_ * zpR[r]) / dzp);
+      if (dzn < 0) b = fmin(b, (-tau_ * znR[r]) / dzn);
+    }
+    return fmin(a, wmin(b));
+  }
+
   // primal fraction to the boundary (oracle frac_to_bound)
   __device__ __forceinline__ double frac_to_bound(double tau_, const GLB double* dUs, const GLB double* dss) const {
     STAMP0();
@@ -1178,6 +1331,480 @@ struct Solver {
 };
 
 // ------------------------------------------------------------------ kernel
+// Feasibility restoration phase (BacktrackingLineSearch -> RestoMinC_1Nrm; oracle
+// restoration()).  Runs between passes of the main iteration loop (which breaks
+// out to it), so none of the main loop's temporaries are live here.  It rebuilds
+// its own view of the scenario's workspace and exchanges only scalars.
+struct RestoIO {
+  double mu0, tau0, theta0, phi0, f, df;
+  int nfilt, nzx, nzs, it, status;
+  double* trace;
+};
+
+template <class CAP>
+__device__ __forceinline__ void resto_phase(const Params* __restrict__ prm, double* ws, int b, RestoIO& io) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  Solver<CAP> S;
+  S.bind(prm, smem, ws, threadIdx.x, b);
+  S.df = io.df; S.nfilt = io.nfilt; S.nzx = io.nzx; S.nzs = io.nzs; S.delta = 0.0;
+  S.mu = io.mu0; S.tau = io.tau0;
+  const nmpc_options& o = prm->o;
+  const int N = S.N, nw = S.nw, ng = S.ng, m = S.m;
+  const int max_iter = o.max_iter;
+  const double smax = o.s_max;
+  double* trace = io.trace;
+  int it = io.it;
+  const double eps = 2.220446049250313e-16;
+  // loop-carried scalars live in LDS (volatile: one LDS access per use) rather than in
+  // registers across the Riccati / rollout calls: restoration is rare, registers are not
+  volatile LDS double* V = S.rvars;
+  auto cmp_le = [&](double lhs, double rhs, double bas) { return lhs - rhs <= 10.0 * eps * fabs(bas); };
+  (void)N;
+      V[0] = io.mu0; V[1] = io.tau0; V[2] = io.theta0; V[3] = io.phi0;
+      const double rho = o.resto_penalty_parameter;
+      const double kd = o.kappa_d, ks = o.kappa_sigma;
+      S.rho = rho;
+      // x_R and the original multipliers; initial mu, p, n and capped multipliers
+      double cmax = 0.0;
+      for (int i = S.lanef(); i < nw; i += WAVE) {
+        S.UR[i] = S.U[i]; S.zl0[i] = S.zl[i]; S.zu0[i] = S.zu[i];
+      }
+      for (int r = S.lanef(); r < ng; r += WAVE) {
+        S.s0[r] = S.s[r]; S.vl0[r] = S.vl[r]; S.vu0[r] = S.vu[r];
+        cmax = fmax(cmax, fabs(S.d[r] - S.s[r]));
+      }
+      V[4] = fmax(V[0], wmax(cmax));
+      V[5] = fmax(o.tau_min, 1.0 - V[4]);
+      S.mu = V[4];
+      S.etaR = o.resto_proximity_weight * sqrt(V[4]);
+      for (int r = S.lanef(); r < ng; r += WAVE) {
+        const double c = S.d[r] - S.s[r];
+        const double qa = V[4] / (2.0 * rho) - 0.5 * c, qb = c * V[4] / (2.0 * rho);
+        const double nv = qa + sqrt(qa * qa + qb), pv = c + nv;
+        S.pR[r] = pv; S.nR[r] = nv; S.zpR[r] = V[4] / pv; S.znR[r] = V[4] / nv;
+        S.vl[r] = S.hasl(S.dl[r]) ? fmin(rho, S.vl[r]) : 0.0;
+        S.vu[r] = S.hasu(S.du[r]) ? fmin(rho, S.vu[r]) : 0.0;
+      }
+      for (int i = S.lanef(); i < nw; i += WAVE) {
+        S.zl[i] = S.hasl(S.xl[i]) ? fmin(rho, S.zl[i]) : 0.0;
+        S.zu[i] = S.hasu(S.xu[i]) ? fmin(rho, S.zu[i]) : 0.0;
+      }
+      sync();
+      // least-squares multipliers of the restoration NLP
+      {
+        bool zero = true;
+        if (o.constr_mult_init_max > 0 && ng > 0) {
+          for (int i = S.lanef(); i < nw; i += WAVE) { S.sigx[i] = 1.0; S.ru[i] = S.zl[i] - S.zu[i]; }
+          S.delta = 0.0;
+          S.assemble(SUM_LS_RESTO, 0.0, 0.0, false);
+          S.riccati(S.sigx, S.ru);
+          S.forward(S.dU, S.dX);
+          double ymax = 0.0;
+          for (int r = S.lanef(); r < ng; r += WAVE) {
+            const int k = r / m, i = r - k * m;
+            const LDS double* xk = S.X + k * 8;
+            const LDS double* dxk = S.dX + k * 8;
+            double jd;
+            if (i < 5) jd = S.dc[r] * dxk[boxidx(i)];
+            else {
+              const int q = i - 5;
+              const double ddx = xk[0] - S.obx[q], ddy = xk[1] - S.oby[q];
+              const double dd = sqrt(ddx * ddx + ddy * ddy);
+              jd = S.dc[r] * ((-(ddx / dd)) * dxk[0] + (-(ddy / dd)) * dxk[1]);
+            }
+            const double yv = ((S.vu[r] - S.vl[r]) + (rho - S.zpR[r]) - (rho - S.znR[r]) - jd) / 3.0;
+            S.y[r] = yv;
+            ymax = fmax(ymax, fabs(yv));
+          }
+          ymax = wmax(ymax);
+          sync();
+          zero = !(ymax <= o.constr_mult_init_max);
+        }
+        if (zero) {
+          for (int r = S.lanef(); r < ng; r += WAVE) S.y[r] = 0.0;
+          sync();
+        }
+      }
+      // the restoration problem's own filter
+      GLB double* ofilt = S.filt;
+      const int onf = S.nfilt;
+      S.filt = S.filtR;
+      S.nfilt = 0;
+      V[6] = -1.0; V[7] = -1.0; V[8] = 0.0; V[9] = 0.0;
+      bool firstR = true;
+      int raccc = 0, rlast_it = -1;
+      V[10] = -1e50; V[11] = -1e50;
+      V[12] = io.f;            // original (scaled) objective at the restoration iterate
+      int rstat = 1;        // 1 running, 0 back to the original problem, else final status
+      while (true) {
+        // ---- progress w.r.t. the original problem (RestoConvergenceCheck)
+        if (!firstR) {
+          double tho = 0.0;
+          for (int r = S.lanef(); r < ng; r += WAVE) tho += fabs(S.d[r] - S.s[r]);
+          tho = wsum(tho);
+          S.mu = V[0];
+          const double pho = S.barrier_obj(V[12], S.U, S.s, nullptr, 0.0);
+          S.mu = V[4];
+          if (tho <= o.required_infeasibility_reduction * V[2] && isfinite(pho)) {
+            const bool ok = cmp_le(tho, (1.0 - o.gamma_theta) * V[2], V[2]) ||
+                            cmp_le(pho - V[3], -o.gamma_phi * V[2], V[3]);
+            if (ok) {
+              GLB double* rf = S.filt;
+              const int rn_ = S.nfilt;
+              S.filt = ofilt; S.nfilt = onf;
+              const bool fok = S.filter_ok(pho, tho);
+              S.filt = rf; S.nfilt = rn_;
+              if (fok) { rstat = 0; break; }
+            }
+          }
+        }
+        // ---- the restoration NLP's own optimality error / termination
+        S.adjoint(0.0, S.y);
+        double dinf = 0, cv = 0, cmr = 0, ucv = 0, sumy = 0, sumz = 0, sumv = 0, sump = 0, frp = 0, frx = 0;
+        bool bad = false;
+        for (int i = S.lanef(); i < nw; i += WAVE) {
+          const double dd = S.U[i] - S.UR[i];
+          const double g = S.grad_u(i) + S.etaR * S.dr2(i) * dd - S.zl[i] + S.zu[i];
+          if (!isfinite(g)) bad = true;
+          dinf = fmax(dinf, fabs(g));
+          if (S.hasl(S.xl[i])) cmr = fmax(cmr, fabs((S.U[i] - S.xl[i]) * S.zl[i]));
+          if (S.hasu(S.xu[i])) cmr = fmax(cmr, fabs((S.xu[i] - S.U[i]) * S.zu[i]));
+          sumz += fabs(S.zl[i]) + fabs(S.zu[i]);
+          frx += S.dr2(i) * dd * dd;
+        }
+        for (int r = S.lanef(); r < ng; r += WAVE) {
+          const double yr = S.y[r], pr = S.pR[r], nr = S.nR[r];
+          dinf = fmax(dinf, fmax(fabs(-yr - S.vl[r] + S.vu[r]), fmax(fabs(rho - yr - S.zpR[r]), fabs(rho + yr - S.znR[r]))));
+          const double drr = S.d[r] - pr + nr;
+          double c1 = 0.0, c2 = 0.0;
+          if (S.hasl(S.dl[r])) {
+            c1 = fmax(c1, S.dl[r] - drr);
+            cmr = fmax(cmr, fabs((S.s[r] - S.dl[r]) * S.vl[r]));
+            c2 = fmax(c2, S.dl[r] - S.d[r]);
+          }
+          if (S.hasu(S.du[r])) {
+            c1 = fmax(c1, drr - S.du[r]);
+            cmr = fmax(cmr, fabs((S.du[r] - S.s[r]) * S.vu[r]));
+            c2 = fmax(c2, S.d[r] - S.du[r]);
+          }
+          cmr = fmax(cmr, fmax(fabs(pr * S.zpR[r]), fabs(nr * S.znR[r])));
+          cv = fmax(cv, c1);
+          ucv = fmax(ucv, c2 / S.dc[r]);
+          sumy += fabs(yr);
+          sumv += fabs(S.vl[r]) + fabs(S.vu[r]);
+          sump += fabs(S.zpR[r]) + fabs(S.znR[r]);
+          frp += pr + nr;
+          if (!isfinite(S.d[r])) bad = true;
+        }
+        dinf = wmax(dinf); cv = wmax(cv); cmr = wmax(cmr); ucv = wmax(ucv);
+        sumy = wsum(sumy); sumz = wsum(sumz); sumv = wsum(sumv); sump = wsum(sump);
+        frp = wsum(frp); frx = wsum(frx);
+        const int ndR = ng + S.nzx + S.nzs + 2 * ng, ncR = S.nzx + S.nzs + 2 * ng;
+        V[13] = fmax(smax, (sumy + sumz + sumv + sump) / ndR) / smax;
+        V[14] = fmax(smax, (sumz + sumv + sump) / ncR) / smax;
+        const double errR = fmax(fmax(dinf / V[13], cv), cmr / V[14]);
+        if (wany(bad) || !isfinite(errR)) { rstat = ST_INVALID_NUMBER; break; }
+        const bool conv = errR <= o.tol && dinf <= o.dual_inf_tol && cv <= o.constr_viol_tol && cmr <= o.compl_inf_tol;
+        if (it != rlast_it) { V[10] = V[11]; V[11] = rho * frp + 0.5 * S.etaR * frx; rlast_it = it; }
+        const bool racc = errR <= o.acceptable_tol && dinf <= o.acceptable_dual_inf_tol &&
+                          cv <= o.acceptable_constr_viol_tol && cmr <= o.acceptable_compl_inf_tol &&
+                          fabs(V[11] - V[10]) / fmax(1.0, fabs(V[11])) <= o.acceptable_obj_change_tol;
+        if (o.acceptable_iter > 0 && racc) ++raccc; else raccc = 0;
+        if (conv || (o.acceptable_iter > 0 && raccc >= o.acceptable_iter)) {
+          rstat = (ucv > o.constr_viol_tol) ? ST_INFEASIBLE : 0;
+          break;
+        }
+        if (it >= max_iter) { rstat = ST_MAXITER; break; }
+        firstR = false;
+        // ---- monotone barrier update of the restoration problem
+        {
+          // barrier error at a candidate mu (the proximity weight eta depends on mu)
+          auto sub_errR = [&](double mu_) {
+            const double et = o.resto_proximity_weight * sqrt(mu_);
+            double dn = 0.0, cm = 0.0, pinf = 0.0;
+            for (int i = S.lanef(); i < nw; i += WAVE) {
+              const double g = S.grad_u(i) + et * S.dr2(i) * (S.U[i] - S.UR[i]) - S.zl[i] + S.zu[i];
+              dn = fmax(dn, fabs(g));
+              if (S.hasl(S.xl[i])) cm = fmax(cm, fabs((S.U[i] - S.xl[i]) * S.zl[i] - mu_));
+              if (S.hasu(S.xu[i])) cm = fmax(cm, fabs((S.xu[i] - S.U[i]) * S.zu[i] - mu_));
+            }
+            for (int r = S.lanef(); r < ng; r += WAVE) {
+              const double yr = S.y[r];
+              dn = fmax(dn, fmax(fabs(-yr - S.vl[r] + S.vu[r]),
+                                 fmax(fabs(rho - yr - S.zpR[r]), fabs(rho + yr - S.znR[r]))));
+              if (S.hasl(S.dl[r])) cm = fmax(cm, fabs((S.s[r] - S.dl[r]) * S.vl[r] - mu_));
+              if (S.hasu(S.du[r])) cm = fmax(cm, fabs((S.du[r] - S.s[r]) * S.vu[r] - mu_));
+              cm = fmax(cm, fmax(fabs(S.pR[r] * S.zpR[r] - mu_), fabs(S.nR[r] * S.znR[r] - mu_)));
+              pinf = fmax(pinf, fabs(S.d[r] - S.s[r] - S.pR[r] + S.nR[r]));
+            }
+            return fmax(fmax(wmax(dn) / V[13], wmax(pinf)), wmax(cm) / V[14]);
+          };
+          double se = sub_errR(V[4]);
+          bool done = false;
+          while (se <= o.barrier_tol_factor * V[4] && !done) {
+            double nmu = fmin(o.kappa_mu * V[4], pow(V[4], o.theta_mu));
+            nmu = fmax(nmu, fmin(o.tol, o.compl_inf_tol) / (o.barrier_tol_factor + 1.0));
+            const bool changed = nmu != V[4];
+            V[4] = nmu;
+            V[5] = fmax(o.tau_min, 1.0 - V[4]);
+            if (!changed) done = true;
+            else {
+              se = sub_errR(V[4]);
+              done = se > o.barrier_tol_factor * V[4];
+            }
+            if (done && changed) S.nfilt = 0;
+          }
+          S.mu = V[4];
+          S.etaR = o.resto_proximity_weight * sqrt(V[4]);
+        }
+        // ---- Newton step of the restoration problem (p, n eliminated per row)
+        for (int i = S.lanef(); i < nw; i += WAVE) {
+          const bool hl = S.hasl(S.xl[i]), hu = S.hasu(S.xu[i]);
+          const double Sl = hl ? S.U[i] - S.xl[i] : 1.0, Su = hu ? S.xu[i] - S.U[i] : 1.0;
+          const double w2 = S.etaR * S.dr2(i);
+          S.sigx[i] = w2 + ((hl ? S.zl[i] / Sl : 0.0) + (hu ? S.zu[i] / Su : 0.0));
+          S.ru[i] = w2 * (S.U[i] - S.UR[i]) + (-(hl ? V[4] / Sl : 0.0) + (hu ? V[4] / Su : 0.0) +
+                    kd * V[4] * ((hl && !hu ? 1.0 : 0.0) - (hu && !hl ? 1.0 : 0.0)));
+        }
+        sync();
+        if (V[9] > 0) V[8] = V[9];
+        double dR = 0.0;
+        bool fok = false;
+        while (true) {
+          S.delta = dR;
+          S.assemble(SUM_RESTO, 0.0, 0.0, true);
+          if (S.riccati(S.sigx, S.ru)) { fok = true; break; }
+          sync();
+          if (dR == 0.0) dR = (V[8] == 0.0) ? o.first_hessian_perturbation
+                                              : fmax(o.min_hessian_perturbation, V[8] * o.perturb_dec_fact);
+          else if (V[8] == 0.0 || 1e5 * V[8] < dR) dR *= o.perturb_inc_fact_first;
+          else dR *= o.perturb_inc_fact;
+          if (dR > o.max_hessian_perturbation) break;
+        }
+        V[9] = dR;
+        S.delta = dR;
+        if (!fok) { rstat = ST_STEP_ERR; break; }
+        S.forward(S.dU, S.dX);
+        {
+          double th, g;
+          S.row_step_resto(S.dX, false, S.ds, S.dpR, S.dnR, S.dyR, th, g);
+          for (int i = S.lanef(); i < nw; i += WAVE) g += S.ru[i] * S.dU[i];
+          V[15] = wsum(th);
+          V[16] = wsum(g);
+        }
+        V[17] = S.barrier_obj(0.0, S.U, S.s, nullptr, 0.0) + S.resto_pn_terms(S.U, 0.0, nullptr, nullptr);
+        if (V[6] < 0) {
+          V[6] = o.theta_max_fact * fmax(1.0, V[15]);
+          V[7] = o.theta_min_fact * fmax(1.0, V[15]);
+        }
+        auto r_ftype = [&](double a) {
+          return V[16] < 0.0 && a * pow(-V[16], o.s_phi) > o.delta * pow(V[15], o.s_theta);
+        };
+        auto r_armijo = [&](double a, double ph) { return cmp_le(ph - V[17], o.eta_phi * a * V[16], V[17]); };
+        auto r_check = [&](double a_test, double ph, double th) {
+          if (th > V[6]) return false;
+          bool ok;
+          if (a_test > 0.0 && r_ftype(a_test) && V[15] <= V[7]) ok = r_armijo(a_test, ph);
+          else {
+            ok = true;
+            if (ph > V[17]) {
+              double basval = 1.0;
+              if (fabs(V[17]) > 10.0) basval = log10(fabs(V[17]));
+              if (log10(ph - V[17]) > o.obj_max_inc + basval) ok = false;
+            }
+            ok = ok && (cmp_le(th, (1.0 - o.gamma_theta) * V[15], V[15]) ||
+                        cmp_le(ph - V[17], -o.gamma_phi * V[15], V[17]));
+          }
+          return ok && S.filter_ok(ph, th);
+        };
+        double amin = o.gamma_theta;
+        if (V[16] < 0) {
+          amin = fmin(o.gamma_theta, o.gamma_phi * V[15] / (-V[16]));
+          if (V[15] <= V[7]) amin = fmin(amin, o.delta * pow(V[15], o.s_theta) / pow(-V[16], o.s_phi));
+        }
+        amin *= o.alpha_min_frac;
+        V[18] = S.frac_to_bound_resto(V[5], S.dU, S.ds, S.dpR, S.dnR);
+        double a = V[18];
+        V[19] = 0.0; V[20] = 0.0; V[21] = 0.0;
+        int acc = 0, nsteps = 0;  // acc: 1 regular step, 2 SOC step
+        while (a > amin || nsteps == 0) {
+          double fo_t, ph, th;
+          const bool ok_t = S.trial_resto(a, S.dU, S.ds, S.dpR, S.dnR, fo_t, ph, th);
+          if (ok_t && r_check(a, ph, th)) { acc = 1; V[19] = a; V[20] = fo_t; V[21] = ph; break; }
+          if (ok_t && a == V[18] && V[15] <= th && o.max_soc > 0) {
+            double th_tr = th, th_old = 0.0, a_soc = a;
+            for (int r = S.lanef(); r < ng; r += WAVE) S.cms[r] = S.d[r] - S.s[r] - S.pR[r] + S.nR[r];
+            sync();
+            const GLB double *dsp = S.ds, *dpp = S.dpR, *dnp = S.dnR;
+            int cnt = 0;
+            bool soc_ok = false;
+            while (cnt < o.max_soc && (cnt == 0 || th_tr <= o.kappa_soc * th_old)) {
+              th_old = th_tr;
+              for (int r = S.lanef(); r < ng; r += WAVE) {
+                const double sv = S.s[r] + a_soc * dsp[r], pv = S.pR[r] + a_soc * dpp[r], nv = S.nR[r] + a_soc * dnp[r];
+                S.cms[r] = a_soc * S.cms[r] + (S.dt[r] - sv - pv + nv);
+              }
+              sync();
+              S.assemble(SUM_RESTO_SOC, 0.0, 0.0, true);
+              S.resolve(S.ru);
+              S.forward(S.dU2, S.dX);
+              double t0, t1;
+              S.row_step_resto(S.dX, true, S.ds2, S.dp2R, S.dn2R, S.dy2R, t0, t1);
+              a_soc = S.frac_to_bound_resto(V[5], S.dU2, S.ds2, S.dp2R, S.dn2R);
+              dsp = S.ds2; dpp = S.dp2R; dnp = S.dn2R;
+              double fo2, ph2, th2;
+              if (!S.trial_resto(a_soc, S.dU2, S.ds2, S.dp2R, S.dn2R, fo2, ph2, th2)) break;
+              if (r_check(a, ph2, th2)) { acc = 2; V[19] = a_soc; V[20] = fo2; V[21] = ph2; soc_ok = true; break; }
+              ++cnt;
+              th_tr = th2;
+            }
+            if (soc_ok) break;
+          }
+          a *= o.alpha_red_factor;
+          ++nsteps;
+        }
+        if (acc == 0) { rstat = ST_RESTO_FAIL; break; }  // no restoration inside the restoration phase
+        // filter augmentation (F-type + Armijo steps do not augment)
+        {
+          const GLB double* dUa = (acc == 2) ? S.dU2 : S.dU;
+          const GLB double* dsa = (acc == 2) ? S.ds2 : S.ds;
+          const GLB double* dpa = (acc == 2) ? S.dp2R : S.dpR;
+          const GLB double* dna = (acc == 2) ? S.dn2R : S.dnR;
+          const GLB double* dya = (acc == 2) ? S.dy2R : S.dyR;
+          if (!(r_ftype(a) && r_armijo(a, V[21])))
+            S.filter_add(V[17] - o.gamma_phi * V[15], (1.0 - o.gamma_theta) * V[15]);
+          // ---- accept the restoration trial point
+          const double ad = S.dual_frac_to_bound_resto(V[5], dUa, dsa, dpa, dna);
+          for (int i = S.lanef(); i < nw; i += WAVE) {
+            double dzl, dzu;
+            S.dz_x(i, dUa[i], dzl, dzu);
+            double nzl = S.zl[i] + ad * dzl, nzu = S.zu[i] + ad * dzu;
+            const double un = S.Ut[i];
+            if (S.hasl(S.xl[i])) { const double Sn = un - S.xl[i]; nzl = fmax(fmin(nzl, ks * V[4] / Sn), V[4] / (ks * Sn)); }
+            else nzl = 0.0;
+            if (S.hasu(S.xu[i])) { const double Sn = S.xu[i] - un; nzu = fmax(fmin(nzu, ks * V[4] / Sn), V[4] / (ks * Sn)); }
+            else nzu = 0.0;
+            S.zl[i] = nzl; S.zu[i] = nzu;
+          }
+          for (int r = S.lanef(); r < ng; r += WAVE) {
+            double dvl, dvu;
+            S.dv_s(r, dsa[r], dvl, dvu);
+            const double pr = S.pR[r], nr = S.nR[r];
+            const double dzp = V[4] / pr - S.zpR[r] - (S.zpR[r] / pr) * dpa[r];
+            const double dzn = V[4] / nr - S.znR[r] - (S.znR[r] / nr) * dna[r];
+            const double sn = S.s[r] + V[19] * dsa[r];
+            const double pn = pr + V[19] * dpa[r], nn = nr + V[19] * dna[r];
+            double nvl = S.vl[r] + ad * dvl, nvu = S.vu[r] + ad * dvu;
+            if (S.hasl(S.dl[r])) { const double Sn = sn - S.dl[r]; nvl = fmax(fmin(nvl, ks * V[4] / Sn), V[4] / (ks * Sn)); }
+            else nvl = 0.0;
+            if (S.hasu(S.du[r])) { const double Sn = S.du[r] - sn; nvu = fmax(fmin(nvu, ks * V[4] / Sn), V[4] / (ks * Sn)); }
+            else nvu = 0.0;
+            const double nzp = S.zpR[r] + ad * dzp, nzn = S.znR[r] + ad * dzn;
+            S.zpR[r] = fmax(fmin(nzp, ks * V[4] / pn), V[4] / (ks * pn));
+            S.znR[r] = fmax(fmin(nzn, ks * V[4] / nn), V[4] / (ks * nn));
+            S.y[r] = S.y[r] + V[19] * dya[r];
+            S.vl[r] = nvl; S.vu[r] = nvu;
+            S.s[r] = sn; S.pR[r] = pn; S.nR[r] = nn;
+            S.d[r] = S.dt[r];
+          }
+          for (int i = S.lanef(); i < nw; i += WAVE) S.U[i] = S.Ut[i];
+          if (S.lanef() <= N) {
+#pragma unroll
+            for (int c = 0; c < 8; ++c) S.X[S.lanef() * 8 + c] = S.Xt[S.lanef() * 8 + c];
+          }
+          sync();
+          V[12] = V[20];
+          S.derivs(S.X, S.U);
+          ++it;
+          if (trace && S.lanef() == 0) {
+            double th = 0.0;
+            for (int r = 0; r < ng; ++r) th += fabs(S.d[r] - S.s[r] - S.pR[r] + S.nR[r]);
+            double* t = trace + (long long)(it - 1) * TRACE_F;
+            t[0] = it; t[1] = V[4]; t[2] = V[20]; t[3] = th; t[4] = V[9]; t[5] = V[19]; t[6] = ad;
+            t[7] = -(double)(nsteps + 1);  // negative: a restoration iteration
+          }
+          sync();
+        }
+      }
+      S.filt = ofilt;
+      S.nfilt = onf;
+      S.mu = V[0];
+      S.tau = V[1];
+      io.status = rstat;
+      io.it = it;
+      if (rstat != 0) return;
+      // ---- back to the original problem: bound multipliers by a Newton step for
+      //      complementarity over the whole restoration (fraction to the boundary,
+      //      reset to 1 above bound_mult_reset_threshold); y = 0 (constr_mult_reset_threshold)
+      {
+        double a = 1.0, zmax = 0.0;
+        for (int i = S.lanef(); i < nw; i += WAVE) {
+          if (S.hasl(S.xl[i])) {
+            const double S0 = S.UR[i] - S.xl[i], S1 = S.U[i] - S.xl[i];
+            const double dz = (V[0] - S.zl0[i] * (S1 - S0)) / S0 - S.zl0[i];
+            if (dz < 0) a = fmin(a, (-V[1] * S.zl0[i]) / dz);
+            S.ru[i] = dz;
+          } else S.ru[i] = 0.0;
+          if (S.hasu(S.xu[i])) {
+            const double S0 = S.xu[i] - S.UR[i], S1 = S.xu[i] - S.U[i];
+            const double dz = (V[0] - S.zu0[i] * (S1 - S0)) / S0 - S.zu0[i];
+            if (dz < 0) a = fmin(a, (-V[1] * S.zu0[i]) / dz);
+            S.sigx[i] = dz;
+          } else S.sigx[i] = 0.0;
+        }
+        for (int r = S.lanef(); r < ng; r += WAVE) {
+          if (S.hasl(S.dl[r])) {
+            const double S0 = S.s0[r] - S.dl[r], S1 = S.s[r] - S.dl[r];
+            const double dz = (V[0] - S.vl0[r] * (S1 - S0)) / S0 - S.vl0[r];
+            if (dz < 0) a = fmin(a, (-V[1] * S.vl0[r]) / dz);
+            S.dpR[r] = dz;
+          } else S.dpR[r] = 0.0;
+          if (S.hasu(S.du[r])) {
+            const double S0 = S.du[r] - S.s0[r], S1 = S.du[r] - S.s[r];
+            const double dz = (V[0] - S.vu0[r] * (S1 - S0)) / S0 - S.vu0[r];
+            if (dz < 0) a = fmin(a, (-V[1] * S.vu0[r]) / dz);
+            S.dnR[r] = dz;
+          } else S.dnR[r] = 0.0;
+        }
+        a = wmin(a);
+        sync();
+        for (int i = S.lanef(); i < nw; i += WAVE) {
+          S.zl[i] = S.zl0[i] + a * S.ru[i];
+          S.zu[i] = S.zu0[i] + a * S.sigx[i];
+          zmax = fmax(zmax, fmax(fabs(S.zl[i]), fabs(S.zu[i])));
+        }
+        for (int r = S.lanef(); r < ng; r += WAVE) {
+          S.vl[r] = S.vl0[r] + a * S.dpR[r];
+          S.vu[r] = S.vu0[r] + a * S.dnR[r];
+          zmax = fmax(zmax, fmax(fabs(S.vl[r]), fabs(S.vu[r])));
+          S.y[r] = 0.0;
+        }
+        zmax = wmax(zmax);
+        sync();
+        const bool reset = zmax > o.bound_mult_reset_threshold;
+        // kappa_sigma safeguard of the accepted point (IpoptAlgorithm::AcceptTrialPoint)
+        for (int i = S.lanef(); i < nw; i += WAVE) {
+          double nzl = reset ? 1.0 : S.zl[i], nzu = reset ? 1.0 : S.zu[i];
+          if (S.hasl(S.xl[i])) { const double Sn = S.U[i] - S.xl[i]; nzl = fmax(fmin(nzl, ks * V[0] / Sn), V[0] / (ks * Sn)); }
+          else nzl = 0.0;
+          if (S.hasu(S.xu[i])) { const double Sn = S.xu[i] - S.U[i]; nzu = fmax(fmin(nzu, ks * V[0] / Sn), V[0] / (ks * Sn)); }
+          else nzu = 0.0;
+          S.zl[i] = nzl; S.zu[i] = nzu;
+        }
+        for (int r = S.lanef(); r < ng; r += WAVE) {
+          double nvl = reset ? 1.0 : S.vl[r], nvu = reset ? 1.0 : S.vu[r];
+          if (S.hasl(S.dl[r])) { const double Sn = S.s[r] - S.dl[r]; nvl = fmax(fmin(nvl, ks * V[0] / Sn), V[0] / (ks * Sn)); }
+          else nvl = 0.0;
+          if (S.hasu(S.du[r])) { const double Sn = S.du[r] - S.s[r]; nvu = fmax(fmin(nvu, ks * V[0] / Sn), V[0] / (ks * Sn)); }
+          else nvu = 0.0;
+          S.vl[r] = nvl; S.vu[r] = nvu;
+        }
+        sync();
+      }
+      io.f = V[12];
+      io.it = it;
+}
+
 // One scenario's solve (the whole IPOPT loop) by the calling wavefront.
 template <class CAP>
 __device__ __forceinline__ void solve_one(Solver<CAP>& S, const Params* __restrict__ prm, const IO& io, const int b) {
@@ -1377,15 +2004,21 @@ __device__ __forceinline__ void solve_one(Solver<CAP>& S, const Params* __restri
   }
   S.mu = o.mu_init;
   S.tau = fmax(o.tau_min, 1.0 - S.mu);
-  double theta_max = -1.0, theta_min = -1.0;
-  double delta_last = 0.0, delta_curr = 0.0;
-  bool in_soft = false, tiny_flag = false;
+  // loop-carried scalars read a few times per iteration: kept in LDS (slots 24..29 of the
+  // scalar block) instead of registers held across every heavy phase
+  volatile LDS double* MV = S.rvars + 24;
+  MV[0] = -1.0; MV[1] = -1.0;
+  MV[2] = 0.0; MV[3] = 0.0;
+  bool in_soft = false, tiny_flag = false, have_acc = false;
   int soft_cnt = 0, acc_cnt = 0, last_obj_iter = -1;
-  double last_obj = -1e50, curr_obj = -1e50;
+  MV[4] = -1e50; MV[5] = -1e50;
   const double smax = o.s_max;
   bool running = (status == 0);
+  bool need_resto = false;
+  RestoIO rio;
 
   while (running) {
+  while (true) {
     // ===== adjoint with current y (grad of the Lagrangian, Hessian multipliers)
     S.adjoint(S.df, S.y);
     STAMP0();
@@ -1434,16 +2067,21 @@ __device__ __forceinline__ void solve_one(Solver<CAP>& S, const Params* __restri
     if (err <= o.tol && u_dinf <= o.dual_inf_tol && ucviol <= o.constr_viol_tol && u_cmp <= o.compl_inf_tol) {
       status = ST_SUCCESS; break;
     }
-    if (it != last_obj_iter) { last_obj = curr_obj; curr_obj = f; last_obj_iter = it; }
+    if (it != last_obj_iter) { MV[4] = MV[5]; MV[5] = f; last_obj_iter = it; }
     const bool acceptable = err <= o.acceptable_tol && u_dinf <= o.acceptable_dual_inf_tol &&
                             ucviol <= o.acceptable_constr_viol_tol && u_cmp <= o.acceptable_compl_inf_tol &&
-                            fabs(curr_obj - last_obj) / fmax(1.0, fabs(curr_obj)) <= o.acceptable_obj_change_tol;
+                            fabs(MV[5] - MV[4]) / fmax(1.0, fabs(MV[5])) <= o.acceptable_obj_change_tol;
     if (o.acceptable_iter > 0 && acceptable) {
       if (++acc_cnt >= o.acceptable_iter) { status = ST_ACCEPTABLE; break; }
     } else {
       acc_cnt = 0;
     }
     if (it >= max_iter) { status = ST_MAXITER; break; }
+    if (acceptable) {  // BacktrackingLineSearch::StoreAcceptablePoint
+      for (int i = S.lanef(); i < nw; i += WAVE) { S.accU[i] = S.U[i]; S.accZl[i] = S.zl[i]; S.accZu[i] = S.zu[i]; }
+      for (int r = S.lanef(); r < ng; r += WAVE) S.accY[r] = S.y[r];
+      have_acc = true;
+    }
 
     // ===== monotone barrier update (MonotoneMuUpdate::UpdateBarrierParameter)
     {
@@ -1480,7 +2118,7 @@ __device__ __forceinline__ void solve_one(Solver<CAP>& S, const Params* __restri
                 o.kappa_d * mu * ((hl && !hu ? 1.0 : 0.0) - (hu && !hl ? 1.0 : 0.0));
     }
     sync();
-    if (delta_curr > 0) delta_last = delta_curr;
+    if (MV[3] > 0) MV[2] = MV[3];
     double delta = 0.0;
     bool fact_ok = false;
     while (true) {
@@ -1489,15 +2127,15 @@ __device__ __forceinline__ void solve_one(Solver<CAP>& S, const Params* __restri
       if (S.riccati(S.sigx, S.ru)) { fact_ok = true; break; }
       sync();
       if (delta == 0.0) {
-        delta = (delta_last == 0.0) ? o.first_hessian_perturbation
-                                    : fmax(o.min_hessian_perturbation, delta_last * o.perturb_dec_fact);
+        delta = (MV[2] == 0.0) ? o.first_hessian_perturbation
+                                    : fmax(o.min_hessian_perturbation, MV[2] * o.perturb_dec_fact);
       } else {
-        if (delta_last == 0.0 || 1e5 * delta_last < delta) delta *= o.perturb_inc_fact_first;
+        if (MV[2] == 0.0 || 1e5 * MV[2] < delta) delta *= o.perturb_inc_fact_first;
         else delta *= o.perturb_inc_fact;
       }
       if (delta > o.max_hessian_perturbation) break;
     }
-    delta_curr = delta;
+    MV[3] = delta;
     S.delta = delta;
     if (!fact_ok) { status = ST_STEP_ERR; break; }
     S.forward(S.dU, S.dX);
@@ -1524,9 +2162,9 @@ __device__ __forceinline__ void solve_one(Solver<CAP>& S, const Params* __restri
       tiny_msv = wmax(msv);
     }
     const double phi_ref = S.barrier_obj(f, S.U, S.s, nullptr, 0.0);
-    if (theta_max < 0) {
-      theta_max = o.theta_max_fact * fmax(1.0, theta_ref);
-      theta_min = o.theta_min_fact * fmax(1.0, theta_ref);
+    if (MV[0] < 0) {
+      MV[0] = o.theta_max_fact * fmax(1.0, theta_ref);
+      MV[1] = o.theta_min_fact * fmax(1.0, theta_ref);
     }
     const double eps = 2.220446049250313e-16;
     auto cmp_le = [&](double lhs, double rhs, double bas) { return lhs - rhs <= 10.0 * eps * fabs(bas); };
@@ -1544,9 +2182,9 @@ __device__ __forceinline__ void solve_one(Solver<CAP>& S, const Params* __restri
              cmp_le(phit - phi_ref, -o.gamma_phi * theta_ref, phi_ref);
     };
     auto check_accept = [&](double a_test, double phit, double tht) {
-      if (tht > theta_max) return false;
+      if (tht > MV[0]) return false;
       bool ok;
-      if (a_test > 0.0 && is_ftype(a_test) && theta_ref <= theta_min) ok = armijo(a_test, phit);
+      if (a_test > 0.0 && is_ftype(a_test) && theta_ref <= MV[1]) ok = armijo(a_test, phit);
       else ok = acc_iter(phit, tht);
       if (!ok) return false;
       return S.filter_ok(phit, tht);
@@ -1647,7 +2285,7 @@ __device__ __forceinline__ void solve_one(Solver<CAP>& S, const Params* __restri
         double amin = o.gamma_theta;
         if (gbd < 0) {
           amin = fmin(o.gamma_theta, o.gamma_phi * theta_ref / (-gbd));
-          if (theta_ref <= theta_min)
+          if (theta_ref <= MV[1])
             amin = fmin(amin, o.delta * pow(theta_ref, o.s_theta) / pow(-gbd, o.s_phi));
         }
         amin *= o.alpha_min_frac;
@@ -1708,7 +2346,27 @@ __device__ __forceinline__ void solve_one(Solver<CAP>& S, const Params* __restri
         }
       }
     }
-    if (acc_kind == 0) { status = ST_RESTO_FAIL; break; }
+    if (acc_kind == 0) {
+      // ===== feasibility restoration phase (BacktrackingLineSearch -> RestoMinC_1Nrm;
+      //       oracle restoration())
+      if (theta_ref <= 1e-2 * o.tol) {
+        // called at an almost feasible point: back to the last acceptable iterate
+        if (have_acc) {
+          for (int i = S.lanef(); i < nw; i += WAVE) { S.U[i] = S.accU[i]; S.zl[i] = S.accZl[i]; S.zu[i] = S.accZu[i]; }
+          for (int r = S.lanef(); r < ng; r += WAVE) S.y[r] = S.accY[r];
+          sync();
+          status = ST_ACCEPTABLE;
+        } else {
+          status = ST_RESTO_FAIL;
+        }
+        break;
+      }
+      S.filter_add(phi_ref - o.gamma_phi * theta_ref, (1.0 - o.gamma_theta) * theta_ref);
+      rio.mu0 = mu; rio.tau0 = tau; rio.theta0 = theta_ref; rio.phi0 = phi_ref; rio.f = f;
+      rio.df = S.df; rio.nfilt = S.nfilt; rio.nzx = S.nzx; rio.nzs = S.nzs; rio.it = it; rio.trace = trace;
+      need_resto = true;
+      break;  // to the restoration phase below the iteration loop
+    }
 
     // ===== accept the trial point (IpoptAlgorithm::AcceptTrialPoint)
     {
@@ -1765,10 +2423,21 @@ __device__ __forceinline__ void solve_one(Solver<CAP>& S, const Params* __restri
       double th = 0.0;
       for (int r = 0; r < ng; ++r) th += fabs(S.d[r] - S.s[r]);
       double* t = trace + (long long)(it - 1) * TRACE_F;
-      t[0] = it; t[1] = mu; t[2] = f; t[3] = th; t[4] = delta_curr; t[5] = alpha_p; t[6] = alpha_d;
+      t[0] = it; t[1] = mu; t[2] = f; t[3] = th; t[4] = MV[3]; t[5] = alpha_p; t[6] = alpha_d;
       t[7] = ls_trials;
     }
     sync();
+  }
+  if (!need_resto) break;
+  // ===== feasibility restoration phase, then back into the iteration loop
+  need_resto = false;
+  resto_phase<CAP>(prm, S.wsbase, b, rio);
+  S.mu = rio.mu0;
+  S.tau = rio.tau0;
+  it = rio.it;
+  if (rio.status != 0) { status = rio.status; break; }
+  f = rio.f;
+  in_soft = false;
   }
 
   // ---------------- outputs (honor_original_bounds)
@@ -2007,6 +2676,8 @@ void nmpc_default_options(nmpc_options* o) {
   o->first_hessian_perturbation = 1e-4; o->min_hessian_perturbation = 1e-20; o->max_hessian_perturbation = 1e20;
   o->perturb_inc_fact_first = 100.0; o->perturb_inc_fact = 8.0; o->perturb_dec_fact = 1.0 / 3.0;
   o->tiny_step_tol = 10 * 2.220446049250313e-16; o->soft_resto_pderror_reduction_factor = 0.9999;
+  o->resto_penalty_parameter = 1000.0; o->resto_proximity_weight = 1.0; o->required_infeasibility_reduction = 0.9;
+  o->bound_mult_reset_threshold = 1000.0; o->constr_mult_reset_threshold = 0.0;
 }
 
 const char* nmpc_last_error(void) { return g_err.c_str(); }

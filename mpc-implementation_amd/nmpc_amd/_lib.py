@@ -40,6 +40,8 @@ _OPT_DBL = (
     "first_hessian_perturbation", "min_hessian_perturbation", "max_hessian_perturbation",
     "perturb_inc_fact_first", "perturb_inc_fact", "perturb_dec_fact",
     "tiny_step_tol", "soft_resto_pderror_reduction_factor",
+    "resto_penalty_parameter", "resto_proximity_weight", "required_infeasibility_reduction",
+    "bound_mult_reset_threshold", "constr_mult_reset_threshold",
 )
 # IPOPT's option names for the fields whose C name differs
 IPOPT_ALIASES = {

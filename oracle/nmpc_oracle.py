@@ -40,9 +40,12 @@ relaxation, bound push, least-squares constraint-multiplier initialisation,
 monotone (Fiacco-McCormick) barrier update with fast decrease, inertia
 correction on the Hessian block, fraction-to-boundary, filter line search with
 Armijo/F-type switching, second-order corrections, tiny-step detection,
-kappa_sigma multiplier safeguard, soft restoration phase, optimal/acceptable/
-max-iter termination, honor_original_bounds.  NOT restated: the full
-feasibility-restoration NLP (terminates with status -2 instead) and the
+kappa_sigma multiplier safeguard, soft restoration phase, the feasibility
+restoration phase (min rho*sum(p+n) + eta/2*|D_R(x-x_R)|^2 s.t. d(x)-p+n in
+[d_L,d_U], its own filter line search, return test against the original
+filter, bound-multiplier reconstruction), return to the last acceptable point
+when restoration is called at an almost feasible point, optimal/acceptable/
+max-iter/infeasible termination, honor_original_bounds.  NOT restated: the
 watchdog procedure.
 """
 from __future__ import annotations
@@ -438,6 +441,10 @@ IPOPT_DEFAULTS = dict(
     perturb_inc_fact=8.0, perturb_dec_fact=1.0 / 3.0,
     tiny_step_tol=10 * EPS, soft_resto_pderror_reduction_factor=0.9999,
     max_soft_resto_iters=10,
+    # feasibility restoration phase (RestoMinC_1Nrm / RestoIpoptNLP defaults)
+    resto_penalty_parameter=1000.0, resto_proximity_weight=1.0,
+    required_infeasibility_reduction=0.9, bound_mult_reset_threshold=1000.0,
+    constr_mult_reset_threshold=0.0,
 )
 
 # The reference's option dict (Python/NMPC_TT.py:257-265)
@@ -445,6 +452,7 @@ REFERENCE_OPTS = dict(max_iter=100, acceptable_tol=1e-8, acceptable_obj_change_t
 
 # IPOPT ApplicationReturnStatus codes
 SOLVE_SUCCEEDED, SOLVED_TO_ACCEPTABLE_LEVEL, SEARCH_DIRECTION_TOO_SMALL = 0, 1, 3
+INFEASIBLE_PROBLEM_DETECTED = 2
 MAXIMUM_ITERATIONS_EXCEEDED, RESTORATION_FAILED, ERROR_IN_STEP_COMPUTATION = -1, -2, -3
 INVALID_NUMBER_DETECTED = -13
 
@@ -625,6 +633,7 @@ class IpoptDense:
         it = 0
         tr = []
         status = None
+        acc_point = None
 
         def nlp_error(x_, s_, d_, gf_, J_, y_, zl_, zu_, vl_, vu_):
             sd, sc = err_scaling(y_, zl_, zu_, vl_, vu_)
@@ -647,6 +656,379 @@ class IpoptDense:
             nc = nzx + nzs
             cm = np.sum(np.abs(compl(x_, s_, zl_, zu_, vl_, vu_, mu_))) / nc if nc else 0.0
             return dual + prim + cm
+
+        def restoration(x0_, s0_, d0_, ev0_, y0_, zl0_, zu0_, vl0_, vu0_, mu0_, tau0_, theta0_, phi0_,
+                        ofilt, it_, trace_, tr_):
+            """IPOPT's feasibility restoration phase (Waechter & Biegler 2006, sec. 3.3;
+            RestoMinC_1Nrm, RestoIpoptNLP, RestoIterateInitializer, RestoConvergenceCheck)
+            on the scaled problem:  min  rho*sum(p+n) + eta/2*|D_R (x - x_R)|^2,
+            eta = resto_proximity_weight*sqrt(mu_R), D_R = diag(1/max(1,|x_R|)),
+            s.t. d(x) - p + n = s, s in [d_L, d_U], x in [x_L, x_U], p, n >= 0.
+            p and n are eliminated row by row from the Newton system, which keeps the
+            stage structure: each row gets the weight D~ = D/(1 + D(1/Sp + 1/Sn))."""
+            rho = o["resto_penalty_parameter"]
+            xR = x0_.copy()
+            DR2 = (1.0 / np.maximum(1.0, np.abs(xR))) ** 2
+            c0 = d0_ - s0_
+            muR = max(mu0_, amax(c0))
+            tauR = max(o["tau_min"], 1.0 - muR)
+            # initial n, p: minimiser of rho(p+n) - mu ln p - mu ln n s.t. p - n = c, i.e. the
+            # positive root of n^2 - 2a n - b = 0 (RestoIterateInitializer's solve_quadratic)
+            qa = muR / (2.0 * rho) - 0.5 * c0
+            qb = c0 * muR / (2.0 * rho)
+            nn = qa + np.sqrt(qa * qa + qb)
+            pp = c0 + nn
+            xR_, sR = x0_.copy(), s0_.copy()
+            zlR = np.where(xlm, np.minimum(rho, zl0_), 0.0)
+            zuR = np.where(xum, np.minimum(rho, zu0_), 0.0)
+            vlR = np.where(slm, np.minimum(rho, vl0_), 0.0)
+            vuR = np.where(sum_, np.minimum(rho, vu0_), 0.0)
+            zp, zn = muR / pp, muR / nn
+            evR = ev0_
+            dR = d0_
+            JR = dc[:, None] * evR.J
+
+            def eta(mu_):
+                return o["resto_proximity_weight"] * math.sqrt(mu_)
+
+            # least-squares multipliers of the restoration NLP (constr_mult_init_max)
+            yR = np.zeros(m)
+            if o["constr_mult_init_max"] > 0 and m > 0:
+                Jfull = np.hstack([JR, -np.eye(m), np.eye(m)])
+                bx = np.concatenate([eta(muR) * DR2 * (xR_ - xR) - zlR + zuR, rho - zp, rho - zn])
+                bs = vuR - vlR
+                wx = np.linalg.solve(np.eye(n + 2 * m) + Jfull.T @ Jfull, bx + Jfull.T @ bs)
+                yR = bs - Jfull @ wx
+                if np.max(np.abs(yR)) > o["constr_mult_init_max"]:
+                    yR = np.zeros(m)
+            nzp = 2 * m  # p, n: lower bounds only
+
+            def fR(x_, p_, n_, mu_):
+                dd = x_ - xR
+                return rho * float(np.sum(p_ + n_)) + 0.5 * eta(mu_) * float(np.sum(DR2 * dd * dd))
+
+            def phiR(x_, s_, p_, n_, mu_):
+                Sxl, Sxu, Ssl, Ssu = slacks(x_, s_)
+                val = fR(x_, p_, n_, mu_)
+                val -= mu_ * (np.sum(np.log(Sxl[xlm])) + np.sum(np.log(Sxu[xum]))
+                              + np.sum(np.log(Ssl[slm])) + np.sum(np.log(Ssu[sum_]))
+                              + np.sum(np.log(p_)) + np.sum(np.log(n_)))
+                val += o["kappa_d"] * mu_ * (np.dot(damp_xl, Sxl * xlm) + np.dot(damp_xu, Sxu * xum)
+                                             + np.dot(damp_sl, Ssl * slm) + np.dot(damp_su, Ssu * sum_)
+                                             + np.sum(p_) + np.sum(n_))
+                return val
+
+            def thetaR(d_, s_, p_, n_):
+                return float(np.sum(np.abs(d_ - s_ - p_ + n_)))
+
+            def errR(x_, s_, d_, J_, p_, n_, y_, zl_, zu_, vl_, vu_, zp_, zn_, mu_, mu_c):
+                """(overall error, dual inf, constraint violation, complementarity) of the resto NLP."""
+                glx = eta(mu_) * DR2 * (x_ - xR) + J_.T @ y_ - zl_ + zu_
+                gls = -y_ - vl_ + vu_
+                glp, gln = rho - y_ - zp_, rho + y_ - zn_
+                dinf_ = max(amax(glx), amax(gls), amax(glp), amax(gln))
+                dr = d_ - p_ + n_
+                cv = amax(np.concatenate([np.maximum(0.0, dl - dr)[slm], np.maximum(0.0, dr - du)[sum_]]))
+                cm = amax(np.concatenate([compl(x_, s_, zl_, zu_, vl_, vu_, mu_c), p_ * zp_ - mu_c, n_ * zn_ - mu_c]))
+                smax = o["s_max"]
+                nd = m + nzx + nzs + nzp
+                sd = (np.sum(np.abs(y_)) + np.sum(np.abs(zl_)) + np.sum(np.abs(zu_)) + np.sum(np.abs(vl_))
+                      + np.sum(np.abs(vu_)) + np.sum(np.abs(zp_)) + np.sum(np.abs(zn_))) / nd
+                sd = max(smax, sd) / smax
+                nc = nzx + nzs + nzp
+                sc = (np.sum(np.abs(zl_)) + np.sum(np.abs(zu_)) + np.sum(np.abs(vl_)) + np.sum(np.abs(vu_))
+                      + np.sum(np.abs(zp_)) + np.sum(np.abs(zn_))) / nc
+                sc = max(smax, sc) / smax
+                return max(dinf_ / sd, cv, cm / sc), dinf_, cv, cm, sd, sc, amax(d_ - s_ - p_ + n_)
+
+            def ftb_R(tau_, x_, s_, p_, n_, dx_, ds_, dp_, dn_):
+                a = frac_to_bound(tau_, x_, s_, dx_, ds_)
+                for S, dS in ((p_, dp_), (n_, dn_)):
+                    sel = dS < 0
+                    if np.any(sel):
+                        a = min(a, float(np.min(-tau_ * S[sel] / dS[sel])))
+                return a
+
+            def dftb_R(tau_, zl_, zu_, vl_, vu_, zp_, zn_, st):
+                a = dual_frac_to_bound(tau_, zl_, zu_, vl_, vu_, st[4], st[5], st[6], st[7])
+                for z_, dz_ in ((zp_, st[8]), (zn_, st[9])):
+                    sel = dz_ < 0
+                    if np.any(sel):
+                        a = min(a, float(np.min(-tau_ * z_[sel] / dz_[sel])))
+                return a
+
+            rfilt = []
+            th_max = th_min = None
+            dlast, dcurr = 0.0, 0.0
+            first = True
+            racc, rlast_obj, rcurr_obj, rlast_it = 0, -1e50, -1e50, -1
+            xx, ss = xR_, sR
+            while True:
+                # ---- progress w.r.t. the original problem (RestoConvergenceCheck)
+                if not first:
+                    th_o = float(np.sum(np.abs(dR - ss)))
+                    f_o = df * evR.F
+                    phi_o = barrier_obj(f_o, xx, ss, mu0_)
+                    if th_o <= o["required_infeasibility_reduction"] * theta0_ and np.isfinite(phi_o):
+                        ok = (_compare_le(th_o, (1.0 - o["gamma_theta"]) * theta0_, theta0_)
+                              or _compare_le(phi_o - phi0_, -o["gamma_phi"] * theta0_, phi0_))
+                        if ok and all(phi_o <= fp or th_o <= ft for fp, ft in ofilt):
+                            break
+                # ---- the restoration NLP's own termination
+                err_r, dinf_r, cv_r, cm_r, _, _, _ = errR(xx, ss, dR, JR, pp, nn, yR, zlR, zuR, vlR, vuR, zp, zn,
+                                                          muR, 0.0)
+                if not np.isfinite(err_r):
+                    return dict(status=INVALID_NUMBER_DETECTED, it=it_, x=xx)
+                conv = (err_r <= o["tol"] and dinf_r <= o["dual_inf_tol"] and cv_r <= o["constr_viol_tol"]
+                        and cm_r <= o["compl_inf_tol"])
+                if it_ != rlast_it:
+                    rlast_obj, rcurr_obj, rlast_it = rcurr_obj, fR(xx, pp, nn, muR), it_
+                racc_ok = (err_r <= o["acceptable_tol"] and dinf_r <= o["acceptable_dual_inf_tol"]
+                           and cv_r <= o["acceptable_constr_viol_tol"] and cm_r <= o["acceptable_compl_inf_tol"]
+                           and abs(rcurr_obj - rlast_obj) / max(1.0, abs(rcurr_obj)) <= o["acceptable_obj_change_tol"])
+                if o["acceptable_iter"] > 0 and racc_ok:
+                    racc += 1
+                else:
+                    racc = 0
+                if conv or (o["acceptable_iter"] > 0 and racc >= o["acceptable_iter"]):
+                    # converged restoration problem: original infeasibility not reducible
+                    if cviol_unscaled(dR, dc, gl_, gu_, slm, sum_) > o["constr_viol_tol"]:
+                        return dict(status=INFEASIBLE_PROBLEM_DETECTED, it=it_, x=xx)
+                    break
+                if it_ >= o["max_iter"]:
+                    return dict(status=MAXIMUM_ITERATIONS_EXCEEDED, it=it_, x=xx)
+                first = False
+                # ---- monotone barrier update of the restoration problem
+                def sub_err(mu_):
+                    e_, _, _, _, sd_, sc_, pinf_ = errR(xx, ss, dR, JR, pp, nn, yR, zlR, zuR, vlR, vuR, zp, zn,
+                                                        mu_, mu_)
+                    glx = eta(mu_) * DR2 * (xx - xR) + JR.T @ yR - zlR + zuR
+                    gls = -yR - vlR + vuR
+                    dinf_ = max(amax(glx), amax(gls), amax(rho - yR - zp), amax(rho + yR - zn))
+                    cm_ = amax(np.concatenate([compl(xx, ss, zlR, zuR, vlR, vuR, mu_), pp * zp - mu_,
+                                               nn * zn - mu_]))
+                    return max(dinf_ / sd_, pinf_, cm_ / sc_)
+                se = sub_err(muR)
+                done = False
+                while se <= o["barrier_tol_factor"] * muR and not done:
+                    new_mu = min(o["kappa_mu"] * muR, muR ** o["theta_mu"])
+                    new_mu = max(new_mu, min(o["tol"], o["compl_inf_tol"]) / (o["barrier_tol_factor"] + 1.0))
+                    changed = new_mu != muR
+                    muR = new_mu
+                    tauR = max(o["tau_min"], 1.0 - muR)
+                    if not changed:
+                        done = True
+                    else:
+                        se = sub_err(muR)
+                        done = se > o["barrier_tol_factor"] * muR
+                    if done and changed:
+                        rfilt = []
+                # ---- Newton step (p, n eliminated per row)
+                Sxl, Sxu, Ssl, Ssu = slacks(xx, ss)
+                SigX = np.where(xlm, zlR / Sxl, 0.0) + np.where(xum, zuR / Sxu, 0.0)
+                SigS = np.where(slm, vlR / Ssl, 0.0) + np.where(sum_, vuR / Ssu, 0.0)
+                Sp, Sn = zp / pp, zn / nn
+                et = eta(muR)
+                gphi = (et * DR2 * (xx - xR) - np.where(xlm, muR / Sxl, 0.0) + np.where(xum, muR / Sxu, 0.0)
+                        + o["kappa_d"] * muR * (damp_xl - damp_xu))
+                rs_ = (-yR - np.where(slm, muR / Ssl, 0.0) + np.where(sum_, muR / Ssu, 0.0)
+                       + o["kappa_d"] * muR * (damp_sl - damp_su))
+                rp = rho - yR - muR / pp + o["kappa_d"] * muR
+                rn = rho + yR - muR / nn + o["kappa_d"] * muR
+                cR = dR - ss - pp + nn
+                Wr = evR.hessian(0.0, dc * yR) + np.diag(et * DR2)
+                if dcurr > 0:
+                    dlast = dcurr
+                delta_ = 0.0
+                fact = None
+                while True:
+                    D_ = SigS + delta_
+                    Spd, Snd = Sp + delta_, Sn + delta_
+                    Dt = D_ / (1.0 + D_ * (1.0 / Spd + 1.0 / Snd))
+                    # row weight D~ = (1/D + 1/Sp + 1/Sn)^-1 (p, n eliminated); written
+                    # without 1/D so rows with no bound (D = 0) stay finite
+                    M = Wr + np.diag(SigX + delta_) + JR.T @ (Dt[:, None] * JR)
+                    try:
+                        fact = np.linalg.cholesky(M)
+                        break
+                    except np.linalg.LinAlgError:
+                        if delta_ == 0.0:
+                            delta_ = (o["first_hessian_perturbation"] if dlast == 0.0
+                                      else max(o["min_hessian_perturbation"], dlast * o["perturb_dec_fact"]))
+                        else:
+                            if dlast == 0.0 or 1e5 * dlast < delta_:
+                                delta_ *= o["perturb_inc_fact_first"]
+                            else:
+                                delta_ *= o["perturb_inc_fact"]
+                        if delta_ > o["max_hessian_perturbation"]:
+                            fact = None
+                            break
+                dcurr = delta_
+                if fact is None:
+                    return dict(status=ERROR_IN_STEP_COMPUTATION, it=it_, x=xx)
+                D_ = SigS + delta_
+                Spd, Snd = Sp + delta_, Sn + delta_
+                den = 1.0 / (1.0 + D_ * (1.0 / Spd + 1.0 / Snd))
+                Dt = D_ * den
+
+                def rdir(c_):
+                    # dy = D~ (J dx + c + rs/D + rp/Sp - rn/Sn), with D~ rs/D = rs * den
+                    Dr = Dt * (c_ + rp / Spd - rn / Snd) + rs_ * den
+                    rhs = -(gphi + JR.T @ (yR + Dr))
+                    dx_ = np.linalg.solve(fact.T, np.linalg.solve(fact, rhs))
+                    jd = JR @ dx_
+                    dy_ = Dt * jd + Dr
+                    dp_ = (dy_ - rp) / Spd
+                    dn_ = (-dy_ - rn) / Snd
+                    ds_ = jd + c_ - dp_ + dn_  # linearised d(x) - s - p + n = 0
+                    dzl_ = np.where(xlm, muR / Sxl - zlR - zlR / Sxl * dx_, 0.0)
+                    dzu_ = np.where(xum, muR / Sxu - zuR + zuR / Sxu * dx_, 0.0)
+                    dvl_ = np.where(slm, muR / Ssl - vlR - vlR / Ssl * ds_, 0.0)
+                    dvu_ = np.where(sum_, muR / Ssu - vuR + vuR / Ssu * ds_, 0.0)
+                    dzp_ = muR / pp - zp - Sp * dp_
+                    dzn_ = muR / nn - zn - Sn * dn_
+                    return dx_, ds_, dy_, dp_, dzl_, dzu_, dvl_, dvu_, dzp_, dzn_, dn_
+
+                stp = rdir(cR)
+                # ---- filter line search on the restoration problem
+                th_ref = thetaR(dR, ss, pp, nn)
+                ph_ref = phiR(xx, ss, pp, nn, muR)
+                gphi_s = (-np.where(slm, muR / Ssl, 0.0) + np.where(sum_, muR / Ssu, 0.0)
+                          + o["kappa_d"] * muR * (damp_sl - damp_su))
+                gpn_p = rho - muR / pp + o["kappa_d"] * muR
+                gpn_n = rho - muR / nn + o["kappa_d"] * muR
+                gbd = float(np.dot(gphi, stp[0]) + np.dot(gphi_s, stp[1]) + np.dot(gpn_p, stp[3])
+                            + np.dot(gpn_n, stp[10]))
+                if th_max is None:
+                    th_max = o["theta_max_fact"] * max(1.0, th_ref)
+                    th_min = o["theta_min_fact"] * max(1.0, th_ref)
+
+                def r_ftype(a):
+                    return gbd < 0.0 and a * (-gbd) ** o["s_phi"] > o["delta"] * th_ref ** o["s_theta"]
+
+                def r_armijo(a, ph):
+                    return _compare_le(ph - ph_ref, o["eta_phi"] * a * gbd, ph_ref)
+
+                def r_acc_iter(ph, th):
+                    if ph > ph_ref:
+                        basval = 1.0
+                        if abs(ph_ref) > 10.0:
+                            basval = math.log10(abs(ph_ref))
+                        if math.log10(ph - ph_ref) > o["obj_max_inc"] + basval:
+                            return False
+                    return (_compare_le(th, (1.0 - o["gamma_theta"]) * th_ref, th_ref)
+                            or _compare_le(ph - ph_ref, -o["gamma_phi"] * th_ref, ph_ref))
+
+                def r_check(a_test, ph, th):
+                    if th > th_max:
+                        return False
+                    if a_test > 0.0 and r_ftype(a_test) and th_ref <= th_min:
+                        ok = r_armijo(a_test, ph)
+                    else:
+                        ok = r_acc_iter(ph, th)
+                    return ok and all(ph <= fp or th <= ft for fp, ft in rfilt)
+
+                def r_trial(a, st):
+                    xt, s_t = xx + a * st[0], ss + a * st[1]
+                    pt, nt = pp + a * st[3], nn + a * st[10]
+                    evt = self._evaluate(xt)
+                    dtt = dc * evt.g
+                    if not np.all(np.isfinite(dtt)):
+                        return None
+                    ph = phiR(xt, s_t, pt, nt, muR)
+                    if not np.isfinite(ph):
+                        return None
+                    return xt, s_t, pt, nt, evt, dtt, ph, thetaR(dtt, s_t, pt, nt)
+
+                amin = o["gamma_theta"]
+                if gbd < 0:
+                    amin = min(o["gamma_theta"], o["gamma_phi"] * th_ref / (-gbd))
+                    if th_ref <= th_min:
+                        amin = min(amin, o["delta"] * th_ref ** o["s_theta"] / (-gbd) ** o["s_phi"])
+                amin *= o["alpha_min_frac"]
+                amax_p = ftb_R(tauR, xx, ss, pp, nn, stp[0], stp[1], stp[3], stp[10])
+                a = amax_p
+                nsteps = 0
+                acc = None
+                while a > amin or nsteps == 0:
+                    tri = r_trial(a, stp)
+                    if tri is not None and r_check(a, tri[6], tri[7]):
+                        acc = (a, stp, tri)
+                        break
+                    if tri is not None and a == amax_p and th_ref <= tri[7] and o["max_soc"] > 0:
+                        th_tr, th_old, a_soc, cms, cnt, cur = tri[7], 0.0, a, cR.copy(), 0, tri
+                        while cnt < o["max_soc"] and (cnt == 0 or th_tr <= o["kappa_soc"] * th_old):
+                            th_old = th_tr
+                            cms = a_soc * cms + (cur[5] - cur[1] - cur[2] + cur[3])
+                            st2 = rdir(cms)
+                            a_soc = ftb_R(tauR, xx, ss, pp, nn, st2[0], st2[1], st2[3], st2[10])
+                            cur = r_trial(a_soc, st2)
+                            if cur is None:
+                                break
+                            if r_check(a, cur[6], cur[7]):
+                                acc = (a_soc, st2, cur)
+                                break
+                            cnt += 1
+                            th_tr = cur[7]
+                        if acc is not None:
+                            break
+                    a *= o["alpha_red_factor"]
+                    nsteps += 1
+                if acc is None:  # no restoration inside the restoration phase
+                    return dict(status=RESTORATION_FAILED, it=it_, x=xx)
+                a_acc, st, tri = acc
+                if not (r_ftype(a) and r_armijo(a, tri[6])):
+                    rfilt.append((ph_ref - o["gamma_phi"] * th_ref, (1.0 - o["gamma_theta"]) * th_ref))
+                ad = dftb_R(tauR, zlR, zuR, vlR, vuR, zp, zn, st)
+                xx, ss, pp, nn, evR, dR = tri[0], tri[1], tri[2], tri[3], tri[4], tri[5]
+                yR = yR + a_acc * st[2]
+                zlR, zuR = zlR + ad * st[4], zuR + ad * st[5]
+                vlR, vuR = vlR + ad * st[6], vuR + ad * st[7]
+                zp, zn = zp + ad * st[8], zn + ad * st[9]
+                Sxl, Sxu, Ssl, Ssu = slacks(xx, ss)
+                ks = o["kappa_sigma"]
+                zlR = np.where(xlm, np.maximum(np.minimum(zlR, ks * muR / Sxl), muR / (ks * Sxl)), 0.0)
+                zuR = np.where(xum, np.maximum(np.minimum(zuR, ks * muR / Sxu), muR / (ks * Sxu)), 0.0)
+                vlR = np.where(slm, np.maximum(np.minimum(vlR, ks * muR / Ssl), muR / (ks * Ssl)), 0.0)
+                vuR = np.where(sum_, np.maximum(np.minimum(vuR, ks * muR / Ssu), muR / (ks * Ssu)), 0.0)
+                zp = np.maximum(np.minimum(zp, ks * muR / pp), muR / (ks * pp))
+                zn = np.maximum(np.minimum(zn, ks * muR / nn), muR / (ks * nn))
+                JR = dc[:, None] * evR.J
+                it_ += 1
+                if trace_:
+                    tr_.append(dict(iter=it_, mu=muR, f=fR(xx, pp, nn, muR), theta=thetaR(dR, ss, pp, nn),
+                                    delta=dcurr, alpha_p=a_acc, alpha_d=ad, ls=nsteps + 1, soc=False, resto=True))
+            # ---- back to the original problem (RestoMinC_1Nrm::PerformRestoration)
+            # bound multipliers: Newton step for complementarity with the primal change
+            # over the whole restoration phase, fraction-to-boundary, reset if large
+            Sxl0, Sxu0, Ssl0, Ssu0 = slacks(x0_, s0_)
+            Sxl1, Sxu1, Ssl1, Ssu1 = slacks(xx, ss)
+
+            def bstep(z_, S0, S1, msk):
+                return np.where(msk, (mu0_ - z_ * (S1 - S0)) / S0 - z_, 0.0)
+
+            dzl_ = bstep(zl0_, Sxl0, Sxl1, xlm)
+            dzu_ = bstep(zu0_, Sxu0, Sxu1, xum)
+            dvl_ = bstep(vl0_, Ssl0, Ssl1, slm)
+            dvu_ = bstep(vu0_, Ssu0, Ssu1, sum_)
+            ad = dual_frac_to_bound(tau0_, zl0_, zu0_, vl0_, vu0_, dzl_, dzu_, dvl_, dvu_)
+            zl1, zu1 = zl0_ + ad * dzl_, zu0_ + ad * dzu_
+            vl1, vu1 = vl0_ + ad * dvl_, vu0_ + ad * dvu_
+            if max(amax(zl1), amax(zu1), amax(vl1), amax(vu1)) > o["bound_mult_reset_threshold"]:
+                zl1, zu1 = np.where(xlm, 1.0, 0.0), np.where(xum, 1.0, 0.0)
+                vl1, vu1 = np.where(slm, 1.0, 0.0), np.where(sum_, 1.0, 0.0)
+            # constraint multipliers: least-squares estimate, ignored above
+            # constr_mult_reset_threshold (default 0: always zero)
+            y1 = np.zeros(m)
+            if o["constr_mult_reset_threshold"] > 0 and m > 0:
+                J1 = dc[:, None] * evR.J
+                bx = df * evR.gradF - zl1 + zu1
+                bs = vu1 - vl1
+                wx = np.linalg.solve(np.eye(n) + J1.T @ J1, bx + J1.T @ bs)
+                y1 = bs - J1 @ wx
+                if np.max(np.abs(y1)) > o["constr_mult_reset_threshold"]:
+                    y1 = np.zeros(m)
+            return dict(status=None, it=it_, x=xx, s=ss, ev=evR, y=y1, zl=zl1, zu=zu1, vl=vl1, vu=vu1)
 
         while True:
             # ---------------- convergence check ----------------
@@ -675,6 +1057,8 @@ class IpoptDense:
             if it >= o["max_iter"]:
                 status = MAXIMUM_ITERATIONS_EXCEEDED
                 break
+            if acceptable:  # BacktrackingLineSearch::StoreAcceptablePoint
+                acc_point = (x.copy(), zl.copy(), zu.copy(), y.copy())
 
             # ---------------- barrier parameter update ----------------
             sub_err = barrier_error(x, s, d, gf, J, y, zl, zu, vl, vu, mu)
@@ -907,8 +1291,26 @@ class IpoptDense:
                         filt.append((phi_ref - o["gamma_phi"] * theta_ref, (1.0 - o["gamma_theta"]) * theta_ref))
 
             if accepted is None:
-                status = RESTORATION_FAILED
-                break
+                # feasibility restoration phase (BacktrackingLineSearch -> RestoMinC_1Nrm)
+                if theta_ref <= 1e-2 * o["tol"]:
+                    # called at an almost feasible point: return the last acceptable iterate
+                    if acc_point is not None:
+                        x, zl, zu, y = acc_point
+                        status = SOLVED_TO_ACCEPTABLE_LEVEL
+                    else:
+                        status = RESTORATION_FAILED
+                    break
+                filt.append((phi_ref - o["gamma_phi"] * theta_ref, (1.0 - o["gamma_theta"]) * theta_ref))
+                rres = restoration(x, s, d, ev, y, zl, zu, vl, vu, mu, tau, theta_ref, phi_ref, filt, it, trace, tr)
+                it = rres["it"]
+                if rres["status"] is not None:
+                    status = rres["status"]
+                    x = rres["x"]
+                    break
+                x, s, ev, y, zl, zu, vl, vu = (rres[k] for k in ("x", "s", "ev", "y", "zl", "zu", "vl", "vu"))
+                f, d = df * ev.F, dc * ev.g
+                in_soft_resto = False
+                accepted = ("resto",)
 
             if accepted[0] == "reg":
                 _, alpha_p, stp, tri = accepted
@@ -917,8 +1319,10 @@ class IpoptDense:
                 y = y + alpha_p * stp[2]
                 zl, zu = zl + alpha_d * stp[3], zu + alpha_d * stp[4]
                 vl, vu = vl + alpha_d * stp[5], vu + alpha_d * stp[6]
-            else:
+            elif accepted[0] == "soft":
                 (_, alpha_p, alpha_d, x, s, ev, f, d, y, zl, zu, vl, vu, _) = accepted
+            else:
+                alpha_p = alpha_d = 1.0
             # kappa_sigma safeguard (IpoptAlgorithm::correct_bound_multiplier)
             Sxl, Sxu, Ssl, Ssu = slacks(x, s)
             ks = o["kappa_sigma"]
@@ -928,8 +1332,9 @@ class IpoptDense:
             vu = np.where(sum_, np.maximum(np.minimum(vu, ks * mu / Ssu), mu / (ks * Ssu)), 0.0)
             gf = df * ev.gradF
             J = dc[:, None] * ev.J
-            it += 1
-            if trace:
+            if accepted[0] != "resto":  # restoration iterations were counted as they ran
+                it += 1
+            if trace and accepted[0] != "resto":
                 tr.append(dict(iter=it, mu=mu, f=f, theta=float(np.sum(np.abs(d - s))), delta=delta_curr,
                                alpha_p=alpha_p, alpha_d=alpha_d, ls=ls_trials, soc=soc_taken))
 

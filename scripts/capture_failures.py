@@ -1,0 +1,29 @@
+"""Dev tool: run the bench's closed loop per step and save the (warm start, p)
+inputs of solves that end in Restoration_Failed, for replay in the oracle."""
+import os, sys
+import numpy as np, torch
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "mpc-implementation_amd"))
+from nmpc_amd import nlpsol, config_spec, draw_scenarios, REFERENCE_OPTS
+K, B = 12, 4096
+spec = config_spec(3)
+s = nlpsol("solver", "ipopt", spec, REFERENCE_OPTS)
+f64 = dict(dtype=torch.float64, device="cuda")
+bnd = [torch.tensor(v, **f64) for v in spec.bounds()]
+p = torch.tensor(draw_scenarios(spec, B, seed=1003), **f64).contiguous()
+w = torch.zeros(B, spec.nw, **f64)
+out = {"x": torch.empty(B, spec.nw, **f64), "status": torch.empty(B, dtype=torch.int32, device="cuda"),
+       "iters": torch.empty(B, dtype=torch.int32, device="cuda")}
+vt, wt = torch.full((B,), 12.0, **f64), torch.full((B,), 0.01, **f64)
+fails = {"w": [], "p": [], "k": [], "b": [], "iters": []}
+for k in range(K):
+    w_in, p_in = w.clone(), p.clone()
+    s.solve_device(w, *bnd, p, out)
+    s.shift_device(p, out["x"], w, vt, wt)
+    st = out["status"].cpu().numpy()
+    idx = np.nonzero(st == -2)[0][:8]
+    for b in idx:
+        fails["w"].append(w_in[b].cpu().numpy()); fails["p"].append(p_in[b].cpu().numpy())
+        fails["k"].append(k); fails["b"].append(int(b)); fails["iters"].append(int(out["iters"][b]))
+    print(k, "n(-2) =", int((st == -2).sum()))
+np.savez(os.path.join(ROOT, "gpurun_out", "fails.npz"), **{k: np.array(v) for k, v in fails.items()})
