@@ -28,6 +28,7 @@
 #include <cstdint>
 #include <cstdio>
 #include <cstring>
+#include <cstdlib>
 #include <mutex>
 #include <string>
 
@@ -2713,6 +2714,10 @@ int nmpc_create(const nmpc_desc* desc, nmpc_handle** out) {
     int ldsd = 0;
     pick_class(P, &h->kern, &h->loop, &ldsd, &h->ws_doubles);
     h->lds_bytes = ldsd * 8;
+  }
+  if (const char* e = std::getenv("NMPC_LDS_BYTES")) {  // diagnostics: pad LDS to cap workgroups per CU
+    const int want = std::atoi(e);
+    if (want > h->lds_bytes) h->lds_bytes = want;
   }
   if (h->lds_bytes > 160 * 1024) {
     delete h;
