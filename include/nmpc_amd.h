@@ -97,6 +97,10 @@ typedef struct nmpc_desc {
   int32_t obs_x_pidx[NMPC_MAX_OBS];   /* -1 = constant, else index into p (dynamic obstacles) */
   int32_t obs_y_pidx[NMPC_MAX_OBS];
   nmpc_options opts;
+  /* cost weights from p (batched weight sweep; the RL replay of
+   * MATLAB/Race Track 1/MPC.m:1,127 rebuilds nlpsol per weight pair): index
+   * into p, or -1 to use w1 / w2 above */
+  int32_t w1_pidx, w2_pidx;
 } nmpc_desc;
 
 typedef struct nmpc_handle nmpc_handle;
@@ -166,6 +170,9 @@ int nmpc_shift_dev(nmpc_handle* h, int32_t B, double* p, int64_t ld_p,
  * scripts' con_t schedules: ld_tk = 1, ld_tb = 0 for one shared schedule;
  * ld_tk = 0 for constant controls), and records the FOV-centre error
  * |FOV(x0_{k+1}) - xs_k[0:2]| (Python/NMPC_TT.py:397-400,433-437) in fov_hist.
+ * p_step (nullable, K x np with leading dimension ld_ps, shared by all
+ * scenarios) is added to p[11:np] after step k: moving obstacles, e.g. the
+ * +-1 m/step windows of MATLAB/Dynamic Obstacles/Dynamic Obstacle avoidance.m:213-230.
  * DEVICE pointers, enqueued on `stream`.
  *   p   : np x B (ld_p >= np), in/out (advanced K steps)
  *   w   : nw x B (ld nw), in: first warm start; out: the last step's shifted solution
@@ -176,6 +183,7 @@ int nmpc_closed_loop_dev(nmpc_handle* h, int32_t B, int32_t K,
                          const double* lbg, int64_t ld_lbg, const double* ubg, int64_t ld_ubg,
                          double* p, int64_t ld_p, double* w,
                          const double* v_t, const double* w_t, int64_t ld_tk, int64_t ld_tb,
+                         const double* p_step, int64_t ld_ps,
                          double* u_hist, double* x_hist, double* f_hist, double* fov_hist,
                          int32_t* status_hist, int32_t* iters_hist, void* stream);
 

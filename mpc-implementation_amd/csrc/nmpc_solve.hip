@@ -52,6 +52,7 @@ constexpr int ST_SUCCESS = 0, ST_ACCEPTABLE = 1, ST_INFEASIBLE = 2, ST_TINY = 3,
 struct Params {
   int N, m, nobs, np, nw, ng, nX;
   double T, w1, w2, hv, hh;
+  int w1p, w2p;  // cost weights from p (-1: constant)
   double ox[NMPC_MAX_OBS], oy[NMPC_MAX_OBS], orr[NMPC_MAX_OBS];
   int oxp[NMPC_MAX_OBS], oyp[NMPC_MAX_OBS];
   nmpc_options o;
@@ -373,8 +374,8 @@ struct Solver {
     const double xt = pp[8], yt = pp[9];
     const double ex = xt - XE, ey = yt - YE;
     const double dx = x[0] - xt, dy = x[1] - yt;
-    return P->w1 * sqrt(dx * dx + dy * dy) +
-           P->w2 * ((A * (ex * ex) + Bq * ey * ex + C * (ey * ey)) - 1);
+    return rvars[30] * sqrt(dx * dx + dy * dy) +
+           rvars[31] * ((A * (ex * ex) + Bq * ey * ex + C * (ey * ey)) - 1);
   }
 
   __device__ __forceinline__ double row_value(const LDS double* x, int i) const {
@@ -461,7 +462,7 @@ struct Solver {
         const double dd = sqrt(ddx * ddx + ddy * ddy);
         const double idd = 1.0 / dd;
         const double id3 = idd * idd * idd;
-        const double w1 = P->w1, w2 = P->w2;
+        const double w1 = rvars[30], w2 = rvars[31];  // this scenario's cost weights
         // gradient
         double g6[6];
 #pragma unroll
@@ -1827,6 +1828,10 @@ __device__ __forceinline__ void solve_one(Solver<CAP>& S, const Params* __restri
     S.obx[S.lanef()] = prm->oxp[S.lanef()] >= 0 ? S.pp[prm->oxp[S.lanef()]] : prm->ox[S.lanef()];
     S.oby[S.lanef()] = prm->oyp[S.lanef()] >= 0 ? S.pp[prm->oyp[S.lanef()]] : prm->oy[S.lanef()];
   }
+  if (S.lanef() == 0) {  // cost weights (LDS scalar slots 30, 31)
+    S.rvars[30] = prm->w1p >= 0 ? S.pp[prm->w1p] : prm->w1;
+    S.rvars[31] = prm->w2p >= 0 ? S.pp[prm->w2p] : prm->w2;
+  }
   const double brf = o.bound_relax_factor, cvt = o.constr_viol_tol;
   bool invalid = false;
   for (int i = S.lanef(); i < nw; i += WAVE) {
@@ -2498,6 +2503,8 @@ struct Loop {
   long long ld_tk, ld_tb;
   double *u_hist, *x_hist, *f_hist;  // K x B x 6, K x B x 8, K x B (nullable)
   double* fov_hist;                  // K x B FOV-centre error (Python/NMPC_TT.py:397-400,433-437)
+  const double* pstep;               // K x np parameter increments after each step (nullable)
+  long long ld_ps;
   int *st_hist, *it_hist;            // K x B (nullable)
 };
 
@@ -2534,7 +2541,8 @@ __global__ __launch_bounds__(WAVE, NMPC_WAVES_PER_EU) void nmpc_closed_loop_kern
       const int i = l + j * WAVE;
       wn[j] = i < nw ? wb[i + 6 < nw ? i + 6 : i] : 0.0;
     }
-    double pv = l < 11 ? pb[l] : 0.0;
+    const int npar = prm->np;
+    double pv = l < npar ? pb[l] : 0.0;
     const double u0 = l < 6 ? wb[l] : 0.0;
     if (lp.x_hist && l < 8) lp.x_hist[(kb + b) * 8 + l] = pv;
     if (lp.u_hist && l < 6) lp.u_hist[(kb + b) * 6 + l] = u0;
@@ -2553,6 +2561,7 @@ __global__ __launch_bounds__(WAVE, NMPC_WAVES_PER_EU) void nmpc_closed_loop_kern
     sync();
     const double pnew = pv + T * fx;
     if (l < 11) pb[l] = pnew;
+    else if (l < npar && lp.pstep) pb[l] = pv + lp.pstep[k * lp.ld_ps + l];  // moving obstacles etc.
     if (lp.fov_hist) {
       // FOV centre of the new state vs the target before its step
       const double x1 = readlane_d(pnew, 0), y1 = readlane_d(pnew, 1), z1 = readlane_d(pnew, 2);
@@ -2696,12 +2705,16 @@ int nmpc_create(const nmpc_desc* desc, nmpc_handle** out) {
     if (desc->obs_x_pidx[j] >= desc->np || desc->obs_y_pidx[j] >= desc->np)
       return fail(NMPC_E_INVALID, "obstacle parameter index >= np");
   }
+  if (desc->w1_pidx >= desc->np || desc->w2_pidx >= desc->np || desc->w1_pidx < -1 || desc->w2_pidx < -1 ||
+      (desc->w1_pidx >= 0 && desc->w1_pidx < 11) || (desc->w2_pidx >= 0 && desc->w2_pidx < 11))
+    return fail(NMPC_E_INVALID, "weight parameter index must be -1 or in [11, np)");
   nmpc_handle* h = new nmpc_handle();
   Params& P = h->hp;
   std::memset(&P, 0, sizeof(P));
   P.N = desc->N; P.nobs = desc->n_obs; P.m = 5 + desc->n_obs; P.np = desc->np;
   P.nw = 6 * P.N; P.ng = P.m * (P.N + 1); P.nX = 8 * (P.N + 1);
   P.T = desc->T; P.w1 = desc->w1; P.w2 = desc->w2; P.hv = desc->vfov / 2; P.hh = desc->hfov / 2;
+  P.w1p = desc->w1_pidx; P.w2p = desc->w2_pidx;
   for (int j = 0; j < NMPC_MAX_OBS; ++j) {
     P.oxp[j] = -1; P.oyp[j] = -1;
   }
@@ -2906,6 +2919,7 @@ int nmpc_closed_loop_dev(nmpc_handle* h, int32_t B, int32_t K, const double* lbx
                          const double* ubx, int64_t ld_ubx, const double* lbg, int64_t ld_lbg,
                          const double* ubg, int64_t ld_ubg, double* p, int64_t ld_p, double* w,
                          const double* v_t, const double* w_t, int64_t ld_tk, int64_t ld_tb,
+                         const double* p_step, int64_t ld_ps,
                          double* u_hist, double* x_hist, double* f_hist, double* fov_hist,
                          int32_t* status_hist, int32_t* iters_hist, void* stream) {
   if (!h) return fail(NMPC_E_INVALID, "null handle");
@@ -2914,6 +2928,7 @@ int nmpc_closed_loop_dev(nmpc_handle* h, int32_t B, int32_t K, const double* lbx
   if (!lbx || !ubx || !lbg || !ubg || !p || !w || !v_t || !w_t)
     return fail(NMPC_E_INVALID, "required pointer is null");
   if (ld_tk < 0 || ld_tb < 0) return fail(NMPC_E_INVALID, "negative target-schedule stride");
+  if (p_step && ld_ps < 0) return fail(NMPC_E_INVALID, "negative p_step stride");
   const Params& P = h->hp;
   if ((ld_lbx != 0 && ld_lbx < P.nw) || (ld_ubx != 0 && ld_ubx < P.nw) || (ld_lbg != 0 && ld_lbg < P.ng) ||
       (ld_ubg != 0 && ld_ubg < P.ng) || ld_p < P.np)
@@ -2928,6 +2943,7 @@ int nmpc_closed_loop_dev(nmpc_handle* h, int32_t B, int32_t K, const double* lbx
   Loop lp;
   lp.K = K; lp.p = p; lp.ld_p = ld_p; lp.w = w; lp.vt = v_t; lp.wt = w_t; lp.ld_tk = ld_tk; lp.ld_tb = ld_tb;
   lp.u_hist = u_hist; lp.x_hist = x_hist; lp.f_hist = f_hist; lp.fov_hist = fov_hist;
+  lp.pstep = p_step; lp.ld_ps = ld_ps;
   lp.st_hist = status_hist; lp.it_hist = iters_hist;
   hipLaunchKernelGGL(h->loop, dim3(B), dim3(WAVE), h->lds_bytes, (hipStream_t)stream,
                      (const Params*)h->dprm, (int)B, io, lp);

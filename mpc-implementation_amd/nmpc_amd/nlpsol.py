@@ -87,6 +87,7 @@ class Solver:
             d.obs_x[j], d.obs_y[j], d.obs_rsum[j] = ob.x, ob.y, ob.r
             d.obs_x_pidx[j], d.obs_y_pidx[j] = ob.x_pidx, ob.y_pidx
         d.opts = make_options(opts)
+        d.w1_pidx, d.w2_pidx = spec.w1_pidx, spec.w2_pidx
         self.max_iter = int(d.opts.max_iter)
         h = C.c_void_p()
         _lib.check(L.nmpc_create(C.byref(d), C.byref(h)))
@@ -223,13 +224,15 @@ class Solver:
                                     C.c_void_p(stream.cuda_stream)))
 
     def closed_loop_device(self, K: int, lbx, ubx, lbg, ubg, p, w, v_t, w_t, hist: dict | None = None,
-                           stream=None):
+                           stream=None, p_step=None):
         """K closed-loop MPC steps per scenario in one launch (see nmpc_closed_loop_dev).
 
         p (B,np) and w (B,nw) are advanced in place.  Target controls v_t, w_t:
         (B,) per scenario, (1,) shared, (K,1) one schedule for all scenarios
         (targets.schedule), or (K,B).  ``hist`` may hold device tensors
         u (K,B,6), x (K,B,8), f (K,B), fov (K,B), status/iters (K,B) int32.
+        ``p_step`` (K,np), optional: added to p[11:] after each step (moving
+        obstacles, targets.obstacle_steps).
         """
         import torch
 
@@ -268,11 +271,18 @@ class Solver:
             t = hist.get(k)
             return C.c_void_p(t.data_ptr()) if t is not None else C.c_void_p(0)
 
+        ps_ld = 0
+        if p_step is not None:
+            assert p_step.dtype == torch.float64 and p_step.is_cuda and p_step.is_contiguous()
+            assert tuple(p_step.shape) == (K, self.np), (tuple(p_step.shape), (K, self.np))
+            ps_ld = self.np
         if stream is None:
             stream = torch.cuda.current_stream()
         _lib.check(L.nmpc_closed_loop_dev(self._h, B, K, *ins, C.c_void_p(p.data_ptr()), self.np,
                                           C.c_void_p(w.data_ptr()), C.c_void_p(v_t.data_ptr()),
-                                          C.c_void_p(w_t.data_ptr()), ld_tk, ld_tb, op("u"), op("x"),
+                                          C.c_void_p(w_t.data_ptr()), ld_tk, ld_tb,
+                                          C.c_void_p(p_step.data_ptr() if p_step is not None else 0), ps_ld,
+                                          op("u"), op("x"),
                                           op("f"), op("fov"), op("status"), op("iters"),
                                           C.c_void_p(stream.cuda_stream)))
 

@@ -61,6 +61,9 @@ class ProblemSpec:
     hfov: float = 1.0
     np: int = 11
     model: str = "uav8g"
+    # cost weights from p (batched weight sweep): index into p or -1
+    w1_pidx: int = -1
+    w2_pidx: int = -1
 
     @property
     def n_obs(self) -> int:
@@ -95,6 +98,9 @@ class ProblemSpec:
         for o in self.obstacles:
             if o.x_pidx >= self.np or o.y_pidx >= self.np:
                 raise ValueError("obstacle parameter index out of range")
+        for i in (self.w1_pidx, self.w2_pidx):
+            if i != -1 and not (11 <= i < self.np):
+                raise ValueError("weight parameter index must be -1 or in [11, np)")
         if not self.T > 0:
             raise ValueError("T must be positive")
         return self
@@ -116,12 +122,15 @@ class ProblemSpec:
 
 
 def make_spec(layout: str | None = "nmpc_tt", N: int = 15, T: float = 1.0, dynamic: bool = False,
-              obstacles: Sequence[Obstacle] | None = None) -> ProblemSpec:
+              obstacles: Sequence[Obstacle] | None = None, weights_in_p: bool = False) -> ProblemSpec:
     """Spec for a reference scenario family.
 
     layout: one of LAYOUTS (None = no obstacles).  dynamic=True makes the y
     coordinate of obstacles 1-6 parameters p[11:17] (MATLAB/Dynamic Obstacles/
-    Dynamic Obstacle avoidance.m:52,128-133), np = 17.
+    Dynamic Obstacle avoidance.m:52,128-133), np = 17.  weights_in_p=True
+    appends the cost weights (w1, w2) to p, one pair per scenario: the batched
+    form of the RL replay that rebuilds nlpsol per weight pair
+    (MATLAB/Race Track 1/MPC.m:1,127).
     """
     if obstacles is None:
         obstacles = ()
@@ -131,7 +140,10 @@ def make_spec(layout: str | None = "nmpc_tt", N: int = 15, T: float = 1.0, dynam
                 Obstacle(float(x), float(y), UAV_R + r, -1, (11 + j) if (dynamic and j < 6) else -1)
                 for j, (x, y) in enumerate(xy))
     npar = 17 if dynamic else 11
-    return ProblemSpec(N=N, T=T, obstacles=tuple(obstacles), np=npar).validate()
+    w1p = w2p = -1
+    if weights_in_p:
+        w1p, w2p, npar = npar, npar + 1, npar + 2
+    return ProblemSpec(N=N, T=T, obstacles=tuple(obstacles), np=npar, w1_pidx=w1p, w2_pidx=w2p).validate()
 
 
 # SURVEY.md section 8 configurations

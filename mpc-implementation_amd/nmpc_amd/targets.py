@@ -60,3 +60,24 @@ def schedule(name: str, start_iter: int, K: int) -> tuple[np.ndarray, np.ndarray
     (shared by every scenario: pass with ld_tb = 0)."""
     vw = np.array([con_t(name, start_iter + k) for k in range(K)], dtype=np.float64).reshape(K, 2)
     return np.ascontiguousarray(vw[:, 0]), np.ascontiguousarray(vw[:, 1])
+
+
+# MATLAB/Dynamic Obstacles/Dynamic Obstacle avoidance.m:213-230: obstacle j's y
+# coordinate (p[10 + j], j = 1..6) moves by +-1 m per MPC iteration inside a
+# window (both ends exclusive), applied after args.p is formed (:211).
+DYNAMIC_OBSTACLE_WINDOWS = [  # (obstacle j, mpciter > a, mpciter < b, step)
+    (2, 100, 400, -1.0), (3, 200, 500, +1.0), (4, 300, 600, -1.0),
+    (5, 500, 800, +1.0), (6, 600, 900, -1.0), (1, 1000, 1300, +1.0),
+]
+
+
+def obstacle_steps(start_iter: int, K: int, np_: int = 17) -> np.ndarray:
+    """(K, np) increments added to p after MPC iterations start_iter ..
+    start_iter+K-1 (p_step of nmpc_closed_loop_dev), dynamic-obstacle script."""
+    out = np.zeros((K, np_))
+    for k in range(K):
+        it = start_iter + k
+        for j, a, b, dy in DYNAMIC_OBSTACLE_WINDOWS:
+            if a < it < b:
+                out[k, 10 + j] += dy
+    return out

@@ -101,6 +101,9 @@ class Problem:
     vfov: float = 1.0
     hfov: float = 1.0
     np_: int = 11
+    # cost weights taken from p (batched weight sweep): index or -1
+    w1_pidx: int = -1
+    w2_pidx: int = -1
 
     nx = 8
     nu = 6
@@ -132,6 +135,15 @@ class Problem:
     @property
     def ng(self):
         return self.m * (self.N + 1)
+
+    def weighted(self, p):
+        """This problem with w1/w2 read from p where w1_pidx/w2_pidx are set."""
+        if self.w1_pidx < 0 and self.w2_pidx < 0:
+            return self
+        import dataclasses
+        return dataclasses.replace(
+            self, w1=float(p[self.w1_pidx]) if self.w1_pidx >= 0 else self.w1,
+            w2=float(p[self.w2_pidx]) if self.w2_pidx >= 0 else self.w2)
 
     def obstacles(self, p):
         ox = self.obs_x.copy()
@@ -214,6 +226,7 @@ def stage_rows(prob, xk, ox, oy):
 
 
 def objective(prob, w, p):
+    prob = prob.weighted(p)
     X = rollout(prob, unpack_w(prob, w), p[:8])
     return sum(stage_cost(prob, X[:, k], p[8], p[9]) for k in range(prob.N))
 
@@ -354,6 +367,7 @@ class SSEval:
     """
 
     def __init__(self, prob: Problem, w, p):
+        prob = prob.weighted(np.asarray(p, float))
         self.prob = prob
         N, nw = prob.N, prob.nw
         self.p = np.asarray(p, float)

@@ -414,3 +414,70 @@ def test_restoration_phase_against_oracle():
         agree += int(st[b]) == int(G["status"][b])
     print(f"restoration cases: final status agrees with the oracle on {agree}/{B}")
     assert agree >= B // 2
+
+
+def test_weights_from_p_match_oracle_and_constant_solver():
+    """Batched weight sweep (the RL replay rebuilds nlpsol per
+    (w1, w2), MATLAB/Race Track 1/MPC.m:1,127): weights read from p per scenario."""
+    from nmpc_amd import make_spec, draw_scenarios
+
+    spec_w = make_spec("race_track_2", N=10, T=0.2, weights_in_p=True)
+    spec_c = make_spec("race_track_2", N=10, T=0.2)
+    B = 4
+    P = draw_scenarios(spec_c, B, seed=31)
+    W = np.array([[1.0, 2.0], [0.5, 3.0], [2.0, 0.5], [1.0, 2.0]])
+    Pw = np.hstack([P, W])
+    lbx, ubx, lbg, ubg = spec_c.bounds()
+    sw = _solver(spec_w)
+    sol_w = sw(x0=np.zeros(spec_w.nw), lbx=lbx, ubx=ubx, lbg=lbg, ubg=ubg, p=Pw.T)
+    sc = _solver(spec_c)
+    sol_c = sc(x0=np.zeros(spec_c.nw), lbx=lbx, ubx=ubx, lbg=lbg, ubg=ubg, p=P.T)
+    # weight pair (1, 2) is the reference's constant setting (Python/NMPC_TT.py:204-205)
+    for b in (0, 3):
+        np.testing.assert_array_equal(sol_w["x"][:, b], sol_c["x"][:, b])
+    prob = orc.make_problem("race_track_2", N=10, T=0.2)
+    prob.w1_pidx, prob.w2_pidx, prob.np_ = 11, 12, 13
+    ref = orc.IpoptDense(prob, orc.REFERENCE_OPTS)
+    st = sw.stats()["status_code"]
+    for b in (1, 2):
+        r = ref.solve(np.zeros(spec_w.nw), lbx, ubx, lbg, ubg, Pw[b])
+        assert int(st[b]) == r["status"]
+        if r["status"] == 0:
+            assert _rel(sol_w["x"][:, b], r["x"]) <= TOL
+            assert abs(sol_w["f"][0, b] - r["f"]) <= TOL * (1 + abs(r["f"]))
+
+
+def test_closed_loop_moving_obstacles_match_oracle_loop():
+    """Device closed loop with the dynamic-obstacle parameter schedule of
+    MATLAB/Dynamic Obstacles/Dynamic Obstacle avoidance.m:211-230 (obstacle 2
+    starts moving after iteration 100) against the oracle's loop."""
+    import torch
+    from nmpc_amd import make_spec
+    from nmpc_amd.targets import obstacle_steps
+
+    spec = make_spec("dynamic", N=10, T=0.2, dynamic=True)
+    B, K, it0 = 3, 3, 100
+    P, bnd, vt, wt = _closed_loop_inputs(spec, B, 41)
+    f64 = dict(dtype=torch.float64, device="cuda")
+    dp = obstacle_steps(it0, K, spec.np)
+    assert dp[0].sum() == 0 and dp[1, 12] == -1.0  # window opens after iteration 100
+    s = _solver(spec)
+    p = torch.tensor(P, **f64)
+    w = torch.zeros(B, spec.nw, **f64)
+    hist = {"u": torch.empty(K, B, 6, **f64), "status": torch.empty(K, B, dtype=torch.int32, device="cuda")}
+    s.closed_loop_device(K, *bnd, p, w, vt, wt, hist, p_step=torch.tensor(dp, **f64))
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(p[:, 11:].cpu().numpy(), P[:, 11:] + dp.sum(0)[11:])
+    prob, ref = _oracle("dynamic", 10, 0.2, dynamic=True)
+    lbx, ubx, lbg, ubg = spec.bounds()
+    for b in range(B):
+        pk, u0 = P[b].copy(), np.zeros(spec.nw)
+        for k in range(K):
+            r = ref.solve(u0, lbx, ubx, lbg, ubg, pk)
+            assert int(hist["status"][k, b]) == r["status"], (b, k)
+            if r["status"] != 0:
+                break
+            assert _rel(hist["u"][k, b].cpu().numpy(), r["x"][:6]) <= TOL
+            x1, u1, xs1 = orc.shift_timestep(prob, pk[:8], r["x"].reshape(spec.N, 6).T, pk[8:11])
+            pk = np.concatenate([x1, xs1, pk[11:] + dp[k, 11:]])
+            u0 = u1.T.ravel()

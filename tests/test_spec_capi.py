@@ -147,3 +147,21 @@ def test_target_schedules_follow_reference_tables():
     assert list(w[:2]) == [0.0, 0.0] and w[2] == w[3] == -(math.pi / 2) / 24 and (v == 13.0).all()
     for name, tab in SCHEDULES.items():
         assert [k for k, _, _ in tab] == sorted(k for k, _, _ in tab), name
+
+
+def test_dynamic_obstacle_schedule_and_weight_indices():
+    """MATLAB/Dynamic Obstacles/Dynamic Obstacle avoidance.m:213-230 windows;
+    weight parameter indices of the batched weight sweep."""
+    import pytest
+    from nmpc_amd import make_spec
+    from nmpc_amd.targets import obstacle_steps
+    from nmpc_amd.spec import ProblemSpec
+
+    d = obstacle_steps(0, 1400)
+    assert d[:, :11].sum() == 0
+    assert d[100, 12] == 0 and d[101, 12] == -1 and d[399, 12] == -1 and d[400, 12] == 0  # y_o_2
+    assert d[:, 13].sum() == 299 and d[:, 16].sum() == -299 and d[1001, 11] == 1
+    s = make_spec("race_track_2", N=20, T=0.2, weights_in_p=True)
+    assert (s.np, s.w1_pidx, s.w2_pidx) == (13, 11, 12)
+    with pytest.raises(ValueError):
+        ProblemSpec(N=5, np=13, w1_pidx=3).validate()
