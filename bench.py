@@ -149,10 +149,25 @@ def main():
         lb = spec.bounds()
         cpu_res = cpu_baseline(spec, draw_scenarios(spec, B, seed=1000 + args.config), *lb,
                                budget_s=args.cpu_budget)
+    # NMPC_BENCH_BACKEND=gloo rehearses the multi-rank path on one GPU (all ranks on
+    # cuda:0); the measured configuration is one process per GPU over RCCL ("nccl")
+    backend = os.environ.get("NMPC_BENCH_BACKEND", "nccl")
+    dev_idx = local_rank % max(1, torch.cuda.device_count()) if world > 1 else 0
     if world > 1:
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-    dev = torch.device("cuda", local_rank if world > 1 else 0)
+        torch.cuda.set_device(dev_idx)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev_idx))
+        else:
+            dist.init_process_group(backend)
+    dev = torch.device("cuda", dev_idx)
+
+    def all_reduce(t, op):
+        if backend == "nccl":
+            dist.all_reduce(t, op=op)
+        else:
+            h = t.cpu()
+            dist.all_reduce(h, op=op)
+            t.copy_(h)
     # global scenario stream, sliced per rank (results independent of world size)
     P_all = draw_scenarios(spec, B * world, seed=1000 + args.config)
     P = P_all[shard(B * world, world, rank)]
@@ -230,8 +245,8 @@ def main():
         el_t = torch.tensor([elapsed], **f64)
         tot = torch.stack([ht["iters"].sum().double(), torch.tensor(float(B * K), **f64)])
         if world > 1:
-            dist.all_reduce(el_t, op=dist.ReduceOp.MAX)
-            dist.all_reduce(tot, op=dist.ReduceOp.SUM)
+            all_reduce(el_t, dist.ReduceOp.MAX)
+            all_reduce(tot, dist.ReduceOp.SUM)
         sts = ht["status"].cpu().numpy()
         hist = {int(s_): int((sts == s_).sum()) for s_ in np.unique(sts)}
         timed_run.fov = float(ht["fov"].mean().item())

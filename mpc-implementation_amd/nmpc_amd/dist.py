@@ -32,7 +32,9 @@ def gather_rows(local, world: int, group=None):
     out = torch.empty((world * local.shape[0],) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
     if dist.get_backend(group) == "nccl":
         dist.all_gather_into_tensor(out, local, group=group)
-    else:  # gloo (CPU tests)
-        parts = list(out.chunk(world))
-        dist.all_gather(parts, local, group=group)
+    else:  # gloo (CPU tests, single-GPU rehearsal): staged through host memory
+        host = local.cpu()
+        parts = [torch.empty_like(host) for _ in range(world)]
+        dist.all_gather(parts, host, group=group)
+        out.copy_(torch.cat(parts, dim=0))
     return out
