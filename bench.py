@@ -70,7 +70,7 @@ def pmc_traffic(kernel, steps, batch):
 
 def _cpu_worker(args):
     """Solve scenarios rows[i::nproc] cold (u=0) with the oracle until the budget runs out."""
-    i, nproc, layout, N, T, P, lbx, ubx, lbg, ubg, budget_s = args
+    i, nproc, layout, N, T, P, lbx, ubx, lbg, ubg, budget_s, model = args
     import warnings
     from threadpoolctl import threadpool_limits
 
@@ -79,13 +79,13 @@ def _cpu_worker(args):
     sys.path.insert(0, ROOT)
     from oracle import nmpc_oracle as orc
 
-    solver = orc.IpoptDense(orc.make_problem(layout, N=N, T=T), orc.REFERENCE_OPTS)
+    solver = orc.IpoptDense(orc.make_problem(layout, N=N, T=T, model=model), orc.REFERENCE_OPTS)
     t0 = time.perf_counter()
     n = iters = 0
     for row in range(i, P.shape[0], nproc):
         if time.perf_counter() - t0 >= budget_s:
             break
-        r = solver.solve(np.zeros(6 * N), lbx, ubx, lbg, ubg, P[row])
+        r = solver.solve(np.zeros(len(lbx)), lbx, ubx, lbg, ubg, P[row])
         iters += r["iter"]
         n += 1
     return n, iters, time.perf_counter() - t0
@@ -108,7 +108,7 @@ def cpu_baseline(spec_cfg, P, lbx, ubx, lbg, ubg, budget_s=15.0):
     t0 = time.perf_counter()
     with mp.get_context("fork").Pool(nproc) as pool:
         res = pool.map(_cpu_worker, [(i, nproc, layout, spec_cfg.N, spec_cfg.T, sample, lbx, ubx, lbg, ubg,
-                                      budget_s) for i in range(nproc)])
+                                      budget_s, spec_cfg.model) for i in range(nproc)])
     wall = time.perf_counter() - t0
     n = sum(r[0] for r in res)
     iters = sum(r[1] for r in res)

@@ -58,7 +58,13 @@ enum {
   NMPC_E_NOMEM = -3    /* device allocation failed */
 };
 
-enum { NMPC_MODEL_UAV8G = 0 /* 8 states / 6 controls, Python/NMPC_TT.py:94-151 */ };
+enum {
+  NMPC_MODEL_UAV8G = 0, /* 8 states / 6 controls, Python/NMPC_TT.py:94-151; p = [x0(8); xs(3); ...] */
+  NMPC_MODEL_UAV5 = 1   /* no gimbal: 5 states / 3 controls, distance cost, rows [z, theta] (+ obstacles),
+                           MATLAB/Dynamic Obstacles/NMPC_TT.m:26-35,102-111,129-134; w = vec(U) with U
+                           3 x N, p = [x0(5); xs(3); ...], X_out 5 x (N+1); w2 is ignored.
+                           Per-step entry points only (nmpc_shift_dev / nmpc_closed_loop_dev reject it) */
+};
 
 /* IPOPT options honoured by the solver (names and meaning as IPOPT's;
  * nmpc_default_options() fills IPOPT's defaults, the reference overrides
@@ -113,7 +119,8 @@ void nmpc_default_options(nmpc_options* opts);
 int nmpc_create(const nmpc_desc* desc, nmpc_handle** out);
 int nmpc_destroy(nmpc_handle* h);
 
-/* Problem dimensions: nw = 6N, ng = (5+n_obs)(N+1), np, nX = 8(N+1). */
+/* Problem dimensions: nw = nu N, ng = (nb+n_obs)(N+1), np, nX = nx(N+1)
+ * (gimbal model: nu = 6, nb = 5, nx = 8; no-gimbal model: nu = 3, nb = 2, nx = 5). */
 int nmpc_dims(const nmpc_handle* h, int32_t* nw, int32_t* ng, int32_t* np, int32_t* nX);
 
 /* Replaces sol = solver(x0=, lbx=, ubx=, lbg=, ubg=, p=) (Python/NMPC_TT.py:358-365)

@@ -53,6 +53,9 @@ struct Params {
   int N, m, nobs, np, nw, ng, nX;
   double T, w1, w2, hv, hh;
   int w1p, w2p;  // cost weights from p (-1: constant)
+  // model embedding: the no-gimbal model (MATLAB/Dynamic Obstacles/NMPC_TT.m) runs on the
+  // gimbal layout with its controls 3..5 / states 5..7 absent
+  int model, nb, nuE, nwE, nxE, npE;  // box rows per stage, real controls/decision/states, external np
   double ox[NMPC_MAX_OBS], oy[NMPC_MAX_OBS], orr[NMPC_MAX_OBS];
   int oxp[NMPC_MAX_OBS], oyp[NMPC_MAX_OBS];
   nmpc_options o;
@@ -216,6 +219,16 @@ __device__ __forceinline__ int hp(int a, int b) {
 __device__ __forceinline__ int vloc(int i) {
   return i < 3 ? i : (i >= 5 ? i - 2 : -1);
 }
+// model embedding: external (caller-layout) index of an internal
+// decision / parameter entry; -1 for an absent gimbal control or state
+__device__ __forceinline__ int ext_u(const Params* prm, int i) {
+  const int k = i / 6, c = i - 6 * k;
+  return c < prm->nuE ? k * prm->nuE + c : -1;
+}
+__device__ __forceinline__ int ext_p(const Params* prm, int i) {
+  if (prm->model == 0) return i;
+  return i < 5 ? i : (i < 8 ? -1 : i - 3);  // [x0(5); xs(3); ...] -> [x0(8); xs(3); ...]
+}
 __device__ __forceinline__ int boxidx(int i) {  // g rows 0..4: z, theta, x5, x6, x7 (NMPC_TT.py:236-240)
   return i == 0 ? 2 : (i == 1 ? 3 : 3 + i);
 }
@@ -227,7 +240,7 @@ enum SumMode { SUM_NEWTON = 0, SUM_LS = 1, SUM_SOC = 2, SUM_RESTO = 3, SUM_RESTO
 // trace buffer.  Never compiled into the product library.
 enum Phase { PH_ROLLOUT, PH_EVAL, PH_DERIVS, PH_ADJ, PH_SUMM, PH_RIC, PH_RESOLVE, PH_FWD, PH_ROWSTEP,
              PH_BARR, PH_FTB, PH_DFTB, PH_CONV, PH_ACCEPT, PH_INIT, PH_TOTAL,
-             PH_RA, PH_RB, PH_RC, PH_RD, PH_RE, PH_COUNT };
+             PH_RA, PH_RB, PH_RC, PH_RD, PH_RE, PH_SIGX, PH_LSSET, PH_FILT, PH_COUNT };
 #ifdef NMPC_STAMPS
 #define STAMP0() const unsigned long long _ts0 = __builtin_amdgcn_s_memtime()
 #define STAMP1(ph) do { const unsigned long long _ts1 = __builtin_amdgcn_s_memtime(); \
@@ -251,6 +264,7 @@ struct Solver {
   // the main loop (that LICM kept ~200 extra VGPRs live for the whole kernel).
   __device__ __forceinline__ int lanef() const { int x = lane_; asm volatile("" : "+v"(x)); return x; }
   int N, m, nobs, nw, ng;
+  int nb, nuE, nwE;  // box rows per stage; real controls per stage; real decision length
   double T;
   // pointers into LDS
   GLB double* U, *Ut, *dU, *dU2, *zl, *zu, *xl, *xu, *sigx, *ru;
@@ -276,6 +290,7 @@ struct Solver {
     constexpr Lay L = CAP::L;
     P = (const CST Params*)prm; sm = (LDS double*)smem; this->lane_ = lane_; b = b_;
     N = prm->N; m = prm->m; nobs = prm->nobs; nw = prm->nw; ng = prm->ng; T = prm->T;
+    nb = prm->nb; nuE = prm->nuE; nwE = prm->nwE;
     wsbase = wsp;
     GLB double* gw = (GLB double*)(wsp + (long long)b_ * L.wstotal);
     U = gw + L.U; Ut = gw + L.Ut; dU = gw + L.dU; dU2 = gw + L.dU2;
@@ -379,8 +394,8 @@ struct Solver {
   }
 
   __device__ __forceinline__ double row_value(const LDS double* x, int i) const {
-    if (i < 5) return x[boxidx(i)];
-    const int o = i - 5;
+    if (i < nb) return x[boxidx(i)];
+    const int o = i - nb;
     const double ddx = x[0] - obx[o], ddy = x[1] - oby[o];
     return -sqrt(ddx * ddx + ddy * ddy) + P->orr[o];
   }
@@ -525,7 +540,7 @@ struct Solver {
 #pragma unroll
       for (int i = 0; i < 8; ++i) w[i] = ofac * gl[k * 8 + i];
       if (yy) {
-        for (int i = 0; i < 5; ++i) {
+        for (int i = 0; i < nb; ++i) {
           const int r = k * m + i;
           w[boxidx(i)] += dc[r] * yy[r];
         }
@@ -533,7 +548,7 @@ struct Solver {
         double cyv[CAP::mmax - 5];
 #pragma unroll
         for (int o = 0; o < CAP::mmax - 5; ++o) {
-          const int r = k * m + 5 + o;
+          const int r = k * m + nb + o;
           cyv[o] = o < nobs ? dc[r] * yy[r] : 0.0;
         }
 #pragma unroll
@@ -643,7 +658,7 @@ struct Solver {
     if (k <= N) {
       const LDS double* xk = X + k * 8;
       double Qxy0 = 0, Qxy1 = 0, Qxy2 = 0, qx = 0, qy = 0;
-      double Qb[5], qb[5];
+      double Qb[5] = {0, 0, 0, 0, 0}, qb[5] = {0, 0, 0, 0, 0};
       const double kd = P->o.kappa_d;
       for (int i = 0; i < m; ++i) {
         const int r = k * m + i;
@@ -673,11 +688,11 @@ struct Solver {
           Bw = y[r] + D * rd + rs;
           C = y[r] * dc[r];
         }
-        if (i < 5) {
+        if (i < nb) {
           Qb[i] = dc[r] * dc[r] * A;
           qb[i] = dc[r] * Bw;
         } else {
-          const int o = i - 5;
+          const int o = i - nb;
           const double ddx = xk[0] - obx[o], ddy = xk[1] - oby[o];
           const double idd = rsq(ddx * ddx + ddy * ddy);
           const double gx = -(ddx * idd), gy = -(ddy * idd);
@@ -808,7 +823,8 @@ struct Solver {
           } else {
             v = T * (T * Pc[(2 + rR) * 8 + 2 + cR]);
           }
-          if (rR == cR) v += (Rd ? Rd[k * 6 + rR] : 1.0) + delta;
+          // an absent control (model embedding) keeps a unit pivot: zero step, no inertia effect
+          if (rR == cR) v = (rR >= nuE) ? 1.0 : v + ((Rd ? Rd[k * 6 + rR] : 1.0) + delta);
           Rc[tR] = v;
           Rk[k * 21 + tR] = v;
         }
@@ -1019,10 +1035,10 @@ struct Solver {
       const LDS double* xk = X + k * 8;
       const LDS double* dxk = dXs + k * 8;
       double jd;
-      if (i < 5) {
+      if (i < nb) {
         jd = dc[r] * dxk[boxidx(i)];
       } else {
-        const int o = i - 5;
+        const int o = i - nb;
         const double ddx = xk[0] - obx[o], ddy = xk[1] - oby[o];
         const double idd = rsq(ddx * ddx + ddy * ddy);
         jd = dc[r] * ((-(ddx * idd)) * dxk[0] + (-(ddy * idd)) * dxk[1]);
@@ -1046,10 +1062,10 @@ struct Solver {
       const LDS double* xk = X + k * 8;
       const LDS double* dxk = dXs + k * 8;
       double jd;
-      if (i < 5) {
+      if (i < nb) {
         jd = dc[r] * dxk[boxidx(i)];
       } else {
-        const int o = i - 5;
+        const int o = i - nb;
         const double ddx = xk[0] - obx[o], ddy = xk[1] - oby[o];
         const double idd = rsq(ddx * ddx + ddy * ddy);
         jd = dc[r] * ((-(ddx * idd)) * dxk[0] + (-(ddy * idd)) * dxk[1]);
@@ -1104,10 +1120,10 @@ struct Solver {
       const LDS double* xk = X + k * 8;
       const LDS double* dxk = dXs + k * 8;
       double jd;
-      if (i < 5) {
+      if (i < nb) {
         jd = dc[r] * dxk[boxidx(i)];
       } else {
-        const int o = i - 5;
+        const int o = i - nb;
         const double ddx = xk[0] - obx[o], ddy = xk[1] - oby[o];
         const double idd = rsq(ddx * ddx + ddy * ddy);
         jd = dc[r] * ((-(ddx * idd)) * dxk[0] + (-(ddy * idd)) * dxk[1]);
@@ -1265,11 +1281,14 @@ struct Solver {
 
   // filter
   __device__ __forceinline__ bool filter_ok(double phi, double th) const {
+    STAMP0();
     bool ok = true;
     for (int e = lanef(); e < nfilt; e += WAVE) {
       if (!(phi <= filt[2 * e] || th <= filt[2 * e + 1])) ok = false;
     }
-    return !wany(!ok);
+    const bool r = !wany(!ok);
+    STAMP1(PH_FILT);
+    return r;
   }
   __device__ __forceinline__ void filter_add(double phi, double th) {
     // drop entries dominated by the new one, then append (IpFilter::AddEntry);
@@ -1407,9 +1426,9 @@ __device__ __forceinline__ void resto_phase(const Params* __restrict__ prm, doub
             const LDS double* xk = S.X + k * 8;
             const LDS double* dxk = S.dX + k * 8;
             double jd;
-            if (i < 5) jd = S.dc[r] * dxk[boxidx(i)];
+            if (i < S.nb) jd = S.dc[r] * dxk[boxidx(i)];
             else {
-              const int q = i - 5;
+              const int q = i - S.nb;
               const double ddx = xk[0] - S.obx[q], ddy = xk[1] - S.oby[q];
               const double dd = sqrt(ddx * ddx + ddy * ddy);
               jd = S.dc[r] * ((-(ddx / dd)) * dxk[0] + (-(ddy / dd)) * dxk[1]);
@@ -1822,7 +1841,10 @@ __device__ __forceinline__ void solve_one(Solver<CAP>& S, const Params* __restri
   double* trace = io.trace ? io.trace + (long long)b * (max_iter + 3) * TRACE_F : nullptr;
 
   // ---------------- load scenario data
-  for (int i = S.lanef(); i < prm->np; i += WAVE) S.pp[i] = io.p[(long long)b * io.ld_p + i];
+  for (int i = S.lanef(); i < prm->np; i += WAVE) {
+    const int e = ext_p(prm, i);  // external p index (model embedding), -1: absent state = 0
+    S.pp[i] = e >= 0 ? io.p[(long long)b * io.ld_p + e] : 0.0;
+  }
   sync();
   if (S.lanef() < S.nobs) {
     S.obx[S.lanef()] = prm->oxp[S.lanef()] >= 0 ? S.pp[prm->oxp[S.lanef()]] : prm->ox[S.lanef()];
@@ -1835,8 +1857,10 @@ __device__ __forceinline__ void solve_one(Solver<CAP>& S, const Params* __restri
   const double brf = o.bound_relax_factor, cvt = o.constr_viol_tol;
   bool invalid = false;
   for (int i = S.lanef(); i < nw; i += WAVE) {
-    S.U[i] = io.x0[(long long)b * io.ld_x0 + i];
-    const double lo = io.lbx[(long long)b * io.ld_lbx + i], hi = io.ubx[(long long)b * io.ld_ubx + i];
+    const int e = ext_u(prm, i);  // external decision index, -1: absent control (fixed at 0, unbounded)
+    S.U[i] = e >= 0 ? io.x0[(long long)b * io.ld_x0 + e] : 0.0;
+    const double lo = e >= 0 ? io.lbx[(long long)b * io.ld_lbx + e] : -INFINITY;
+    const double hi = e >= 0 ? io.ubx[(long long)b * io.ld_ubx + e] : INFINITY;
     S.xl[i] = lo > -BIGB ? lo - fmin(cvt, brf * fmax(1.0, fabs(lo))) : -INFINITY;
     S.xu[i] = hi < BIGB ? hi + fmin(cvt, brf * fmax(1.0, fabs(hi))) : INFINITY;
     if (lo > hi) invalid = true;
@@ -1883,6 +1907,7 @@ __device__ __forceinline__ void solve_one(Solver<CAP>& S, const Params* __restri
     if (status == 0) {
       const int k = S.lanef();
       double rmax[5 + NMPC_MAX_OBS];
+      const int nb = S.nb;
       for (int i = 0; i < m; ++i) rmax[i] = 0.0;
       if (k <= N && k >= 1) {
         const LDS double* xk = S.X + k * 8;
@@ -1900,14 +1925,16 @@ __device__ __forceinline__ void solve_one(Solver<CAP>& S, const Params* __restri
           // rows z, theta, x5, x6, x7
           rmax[0] = fmax(rmax[0], fmax(fabs(b20), fabs(T * e23)));
           rmax[1] = fmax(rmax[1], fabs(T));
-          rmax[2] = fmax(rmax[2], fabs(T));
-          rmax[3] = fmax(rmax[3], fabs(T));
-          rmax[4] = fmax(rmax[4], fabs(T));
+          if (nb == 5) {  // gimbal rows x5, x6, x7
+            rmax[2] = fmax(rmax[2], fabs(T));
+            rmax[3] = fmax(rmax[3], fabs(T));
+            rmax[4] = fmax(rmax[4], fabs(T));
+          }
           for (int q = 0; q < S.nobs; ++q) {
             const double jv = gxo[q] * b00 + gyo[q] * b10;
             const double jt = T * (gxo[q] * e03 + gyo[q] * e13);
             const double jp = T * (gxo[q] * e04 + gyo[q] * e14);
-            rmax[5 + q] = fmax(rmax[5 + q], fmax(fabs(jv), fmax(fabs(jt), fabs(jp))));
+            rmax[nb + q] = fmax(rmax[nb + q], fmax(fabs(jv), fmax(fabs(jt), fabs(jp))));
           }
           e03 += E03; e04 += E04; e13 += E13; e14 += E14; e23 += E23;
         }
@@ -1980,9 +2007,9 @@ __device__ __forceinline__ void solve_one(Solver<CAP>& S, const Params* __restri
         const LDS double* xk = S.X + k * 8;
         const LDS double* dxk = S.dX + k * 8;
         double jd;
-        if (i < 5) jd = S.dc[r] * dxk[boxidx(i)];
+        if (i < S.nb) jd = S.dc[r] * dxk[boxidx(i)];
         else {
-          const int q = i - 5;
+          const int q = i - S.nb;
           const double ddx = xk[0] - S.obx[q], ddy = xk[1] - S.oby[q];
           const double dd = sqrt(ddx * ddx + ddy * ddy);
           jd = S.dc[r] * ((-(ddx / dd)) * dxk[0] + (-(ddy / dd)) * dxk[1]);
@@ -2116,6 +2143,7 @@ __device__ __forceinline__ void solve_one(Solver<CAP>& S, const Params* __restri
     STAMP1(PH_CONV);
 
     // ===== search direction with inertia correction (PDPerturbationHandler)
+    { STAMP0();
     for (int i = S.lanef(); i < nw; i += WAVE) {
       const bool hl = S.hasl(S.xl[i]), hu = S.hasu(S.xu[i]);
       const double Sl = hl ? S.U[i] - S.xl[i] : 1.0, Su = hu ? S.xu[i] - S.U[i] : 1.0;
@@ -2124,6 +2152,7 @@ __device__ __forceinline__ void solve_one(Solver<CAP>& S, const Params* __restri
                 o.kappa_d * mu * ((hl && !hu ? 1.0 : 0.0) - (hu && !hl ? 1.0 : 0.0));
     }
     sync();
+    STAMP1(PH_SIGX); }
     if (MV[3] > 0) MV[2] = MV[3];
     double delta = 0.0;
     bool fact_ok = false;
@@ -2151,6 +2180,7 @@ __device__ __forceinline__ void solve_one(Solver<CAP>& S, const Params* __restri
     {
       double th, g, msv, mx = 0.0;
       S.row_step_ls(S.dX, mu, th, g, msv);
+      STAMP0();
       for (int i = S.lanef(); i < nw; i += WAVE) {
         const double du_ = S.dU[i];
         g += S.ru[i] * du_;
@@ -2166,6 +2196,7 @@ __device__ __forceinline__ void solve_one(Solver<CAP>& S, const Params* __restri
       gbd = wsum(g);
       tiny_mx = wmax(mx);
       tiny_msv = wmax(msv);
+      STAMP1(PH_LSSET);
     }
     const double phi_ref = S.barrier_obj(f, S.U, S.s, nullptr, 0.0);
     if (MV[0] < 0) {
@@ -2221,7 +2252,7 @@ __device__ __forceinline__ void solve_one(Solver<CAP>& S, const Params* __restri
         if (S.hasl(S.dl[r])) cm += fabs((S.s[r] - S.dl[r]) * S.vl[r] - mu);
         if (S.hasu(S.du[r])) cm += fabs((S.du[r] - S.s[r]) * S.vu[r] - mu);
       }
-      const double nn = (double)(nw + ng);
+      const double nn = (double)(S.nwE + ng);
       const double e_c = wsum(dual) / nn + (ng ? wsum(prim) / ng : 0.0) + (nc ? wsum(cm) / nc : 0.0);
       double ft, phit, tht;
       ++ls_trials;
@@ -2448,23 +2479,30 @@ __device__ __forceinline__ void solve_one(Solver<CAP>& S, const Params* __restri
 
   // ---------------- outputs (honor_original_bounds)
   for (int i = S.lanef(); i < nw; i += WAVE) {
-    const double lo = io.lbx[(long long)b * io.ld_lbx + i], hi = io.ubx[(long long)b * io.ld_ubx + i];
+    const int e = ext_u(prm, i);
+    const double lo = e >= 0 ? io.lbx[(long long)b * io.ld_lbx + e] : -INFINITY;
+    const double hi = e >= 0 ? io.ubx[(long long)b * io.ld_ubx + e] : INFINITY;
     S.Ut[i] = fmin(fmax(S.U[i], lo), hi);
   }
   sync();
   S.rollout(S.Ut, S.Xt);
   const double fo = S.eval_fg(S.Xt, S.dt, nullptr);
   for (int i = S.lanef(); i < nw; i += WAVE) {
-    io.x_out[(long long)b * nw + i] = S.Ut[i];
-    if (io.lam_x) io.lam_x[(long long)b * nw + i] = (S.zu[i] - S.zl[i]) / S.df;
+    const int e = ext_u(prm, i);
+    if (e < 0) continue;
+    io.x_out[(long long)b * S.nwE + e] = S.Ut[i];
+    if (io.lam_x) io.lam_x[(long long)b * S.nwE + e] = (S.zu[i] - S.zl[i]) / S.df;
   }
   for (int r = S.lanef(); r < ng; r += WAVE) {
     if (io.g_out) io.g_out[(long long)b * ng + r] = S.dt[r];
     if (io.lam_g) io.lam_g[(long long)b * ng + r] = S.y[r] * S.dc[r] / S.df;
   }
   if (io.X_out) {
-    const int nX = prm->nX;
-    for (int i = S.lanef(); i < nX; i += WAVE) io.X_out[(long long)b * nX + i] = S.Xt[i];
+    const int nX = prm->nX, nxE = prm->nxE, nXE = nxE * (N + 1);
+    for (int i = S.lanef(); i < nX; i += WAVE) {
+      const int k = i >> 3, c = i & 7;
+      if (c < nxE) io.X_out[(long long)b * nXE + k * nxE + c] = S.Xt[i];
+    }
   }
 #ifdef NMPC_STAMPS
   if (trace) {
@@ -2694,33 +2732,45 @@ const char* nmpc_last_error(void) { return g_err.c_str(); }
 
 int nmpc_create(const nmpc_desc* desc, nmpc_handle** out) {
   if (!desc || !out) return fail(NMPC_E_INVALID, "null argument");
-  if (desc->model != NMPC_MODEL_UAV8G) return fail(NMPC_E_INVALID, "unsupported model");
+  if (desc->model != NMPC_MODEL_UAV8G && desc->model != NMPC_MODEL_UAV5)
+    return fail(NMPC_E_INVALID, "unsupported model");
+  const bool nog = desc->model == NMPC_MODEL_UAV5;
+  const int np_min = nog ? 8 : 11;  // [x0; xs]
   if (desc->N < 1 || desc->N > NMPC_MAX_N) return fail(NMPC_E_INVALID, "N out of range [1,63]");
   if (desc->n_obs < 0 || desc->n_obs > NMPC_MAX_OBS) return fail(NMPC_E_INVALID, "n_obs out of range");
-  if (desc->np < 11 || desc->np > 64) return fail(NMPC_E_INVALID, "np out of range [11,64]");
+  if (desc->np < np_min || desc->np > 61) return fail(NMPC_E_INVALID, "np out of range [8 or 11, 61]");
   if (!(desc->T > 0)) return fail(NMPC_E_INVALID, "T must be positive");
   if (desc->opts.max_iter < 0 || desc->opts.max_iter > FCAP - 1 + 100000)
     return fail(NMPC_E_INVALID, "bad max_iter");
   for (int j = 0; j < desc->n_obs; ++j) {
-    if (desc->obs_x_pidx[j] >= desc->np || desc->obs_y_pidx[j] >= desc->np)
-      return fail(NMPC_E_INVALID, "obstacle parameter index >= np");
+    if (desc->obs_x_pidx[j] >= desc->np || desc->obs_y_pidx[j] >= desc->np ||
+        (desc->obs_x_pidx[j] >= 0 && desc->obs_x_pidx[j] < np_min) ||
+        (desc->obs_y_pidx[j] >= 0 && desc->obs_y_pidx[j] < np_min))
+      return fail(NMPC_E_INVALID, "obstacle parameter index must be -1 or in [np_min, np)");
   }
   if (desc->w1_pidx >= desc->np || desc->w2_pidx >= desc->np || desc->w1_pidx < -1 || desc->w2_pidx < -1 ||
-      (desc->w1_pidx >= 0 && desc->w1_pidx < 11) || (desc->w2_pidx >= 0 && desc->w2_pidx < 11))
-    return fail(NMPC_E_INVALID, "weight parameter index must be -1 or in [11, np)");
+      (desc->w1_pidx >= 0 && desc->w1_pidx < np_min) || (desc->w2_pidx >= 0 && desc->w2_pidx < np_min))
+    return fail(NMPC_E_INVALID, "weight parameter index must be -1 or in [np_min, np)");
+  // parameter indices in the internal (gimbal) layout: [x0(8); xs(3); ...]
+  auto pin = [&](int e) { return (e < 0 || !nog) ? e : e + 3; };
   nmpc_handle* h = new nmpc_handle();
   Params& P = h->hp;
   std::memset(&P, 0, sizeof(P));
-  P.N = desc->N; P.nobs = desc->n_obs; P.m = 5 + desc->n_obs; P.np = desc->np;
-  P.nw = 6 * P.N; P.ng = P.m * (P.N + 1); P.nX = 8 * (P.N + 1);
-  P.T = desc->T; P.w1 = desc->w1; P.w2 = desc->w2; P.hv = desc->vfov / 2; P.hh = desc->hfov / 2;
-  P.w1p = desc->w1_pidx; P.w2p = desc->w2_pidx;
+  P.model = desc->model;
+  P.nb = nog ? 2 : 5;                       // box rows per stage: [z, theta] or [z, theta, x5, x6, x7]
+  P.nuE = nog ? 3 : 6; P.nxE = nog ? 5 : 8;
+  P.N = desc->N; P.nobs = desc->n_obs; P.m = P.nb + desc->n_obs;
+  P.npE = desc->np; P.np = desc->np + (nog ? 3 : 0);
+  P.nw = 6 * P.N; P.nwE = P.nuE * P.N; P.ng = P.m * (P.N + 1); P.nX = 8 * (P.N + 1);
+  // the no-gimbal cost is the distance term alone (MATLAB/Dynamic Obstacles/NMPC_TT.m:102-105)
+  P.T = desc->T; P.w1 = desc->w1; P.w2 = nog ? 0.0 : desc->w2; P.hv = desc->vfov / 2; P.hh = desc->hfov / 2;
+  P.w1p = pin(desc->w1_pidx); P.w2p = nog ? -1 : pin(desc->w2_pidx);
   for (int j = 0; j < NMPC_MAX_OBS; ++j) {
     P.oxp[j] = -1; P.oyp[j] = -1;
   }
   for (int j = 0; j < desc->n_obs; ++j) {
     P.ox[j] = desc->obs_x[j]; P.oy[j] = desc->obs_y[j]; P.orr[j] = desc->obs_rsum[j];
-    P.oxp[j] = desc->obs_x_pidx[j]; P.oyp[j] = desc->obs_y_pidx[j];
+    P.oxp[j] = pin(desc->obs_x_pidx[j]); P.oyp[j] = pin(desc->obs_y_pidx[j]);
   }
   P.o = desc->opts;
   {
@@ -2764,10 +2814,10 @@ int nmpc_destroy(nmpc_handle* h) {
 
 int nmpc_dims(const nmpc_handle* h, int32_t* nw, int32_t* ng, int32_t* np, int32_t* nX) {
   if (!h) return fail(NMPC_E_INVALID, "null handle");
-  if (nw) *nw = h->hp.nw;
+  if (nw) *nw = h->hp.nwE;
   if (ng) *ng = h->hp.ng;
-  if (np) *np = h->hp.np;
-  if (nX) *nX = h->hp.nX;
+  if (np) *np = h->hp.npE;
+  if (nX) *nX = h->hp.nxE * (h->hp.N + 1);
   return NMPC_OK;
 }
 
@@ -2804,8 +2854,8 @@ int nmpc_solve_batch_dev(nmpc_handle* h, int32_t B, const double* x0, int64_t ld
   if (!x0 || !lbx || !ubx || !lbg || !ubg || !p || !x_out)
     return fail(NMPC_E_INVALID, "required pointer is null");
   const Params& P = h->hp;
-  if ((ld_x0 != 0 && ld_x0 < P.nw) || (ld_lbx != 0 && ld_lbx < P.nw) || (ld_ubx != 0 && ld_ubx < P.nw) ||
-      (ld_lbg != 0 && ld_lbg < P.ng) || (ld_ubg != 0 && ld_ubg < P.ng) || (ld_p != 0 && ld_p < P.np))
+  if ((ld_x0 != 0 && ld_x0 < P.nwE) || (ld_lbx != 0 && ld_lbx < P.nwE) || (ld_ubx != 0 && ld_ubx < P.nwE) ||
+      (ld_lbg != 0 && ld_lbg < P.ng) || (ld_ubg != 0 && ld_ubg < P.ng) || (ld_p != 0 && ld_p < P.npE))
     return fail(NMPC_E_INVALID, "leading dimension smaller than the vector length");
   IO io;
   io.x0 = x0; io.lbx = lbx; io.ubx = ubx; io.lbg = lbg; io.ubg = ubg; io.p = p;
@@ -2843,7 +2893,7 @@ int nmpc_solve_batch(nmpc_handle* h, int32_t B, const double* x0, int64_t ld_x0,
   if (!x0 || !lbx || !ubx || !lbg || !ubg || !p || !x_out)
     return fail(NMPC_E_INVALID, "required pointer is null");
   const Params& P = h->hp;
-  const size_t nw = P.nw, ng = P.ng, np = P.np, nX = P.nX;
+  const size_t nw = P.nwE, ng = P.ng, np = P.npE, nX = (size_t)P.nxE * (P.N + 1);
   auto cols = [&](int64_t ld) { return ld == 0 ? (size_t)1 : (size_t)B; };
   auto len = [&](int64_t ld, size_t n) { return ld == 0 ? n : (size_t)(B - 1) * (size_t)ld + n; };
   const size_t n_x0 = len(ld_x0, nw), n_lbx = len(ld_lbx, nw), n_ubx = len(ld_ubx, nw);
@@ -2906,6 +2956,7 @@ int nmpc_shift_dev(nmpc_handle* h, int32_t B, double* p, int64_t ld_p, const dou
   if (!h) return fail(NMPC_E_INVALID, "null handle");
   if (B <= 0) return B == 0 ? NMPC_OK : fail(NMPC_E_INVALID, "B < 0");
   if (!p || !u_sol || !w_out || !v_t || !w_t) return fail(NMPC_E_INVALID, "null pointer");
+  if (h->hp.model != NMPC_MODEL_UAV8G) return fail(NMPC_E_INVALID, "shift: gimbal model only");
   if (ld_p < h->hp.np) return fail(NMPC_E_INVALID, "ld_p < np");
   const int thr = 256;
   hipLaunchKernelGGL(nmpc_shift_kernel, dim3((B + thr - 1) / thr), dim3(thr), 0, (hipStream_t)stream, (int)B,
@@ -2930,6 +2981,7 @@ int nmpc_closed_loop_dev(nmpc_handle* h, int32_t B, int32_t K, const double* lbx
   if (ld_tk < 0 || ld_tb < 0) return fail(NMPC_E_INVALID, "negative target-schedule stride");
   if (p_step && ld_ps < 0) return fail(NMPC_E_INVALID, "negative p_step stride");
   const Params& P = h->hp;
+  if (P.model != NMPC_MODEL_UAV8G) return fail(NMPC_E_INVALID, "closed loop: gimbal model only");
   if ((ld_lbx != 0 && ld_lbx < P.nw) || (ld_ubx != 0 && ld_ubx < P.nw) || (ld_lbg != 0 && ld_lbg < P.ng) ||
       (ld_ubg != 0 && ld_ubg < P.ng) || ld_p < P.np)
     return fail(NMPC_E_INVALID, "leading dimension smaller than the vector length");

@@ -80,7 +80,7 @@ class Solver:
         self.error_on_fail = bool((opts or {}).get("error_on_fail", False))
         L = _lib.lib()
         d = _lib.Desc()
-        d.model = 0
+        d.model = 1 if spec.model == "uav5" else 0
         d.N, d.np, d.n_obs = spec.N, spec.np, spec.n_obs
         d.T, d.w1, d.w2, d.vfov, d.hfov = spec.T, spec.w1, spec.w2, spec.vfov, spec.hfov
         for j, ob in enumerate(spec.obstacles):

@@ -34,9 +34,10 @@ def draw_scenarios(spec: ProblemSpec, B: int, seed: int) -> np.ndarray:
                        rng.uniform(-0.2, 0.2), rng.uniform(-np.pi, np.pi), rng.uniform(-0.4, 0.4),
                        rng.uniform(-0.4, 0.4), rng.uniform(-1.4, 1.4)])
         p = np.zeros(spec.np)
-        p[:8], p[8:11] = x0, (xt, yt, pt)
+        nx = spec.nx  # the no-gimbal model packs x0[:5] (same random stream)
+        p[:nx], p[nx:nx + 3] = x0[:nx], (xt, yt, pt)
         oy = oy0.copy()
-        if spec.np > 11:
+        if spec.np > spec.np_min:
             # dynamic obstacle ys: initial layout +- 300 m (the schedule moves them 300 m)
             for j in range(spec.n_obs):
                 if ydyn[j] >= 0:

@@ -70,13 +70,31 @@ class ProblemSpec:
         return len(self.obstacles)
 
     @property
+    def nu(self) -> int:
+        return 3 if self.model == "uav5" else NU
+
+    @property
+    def nx(self) -> int:
+        return 5 if self.model == "uav5" else NX
+
+    @property
+    def nb(self) -> int:
+        """box rows per stage: z, theta, x5, x6, x7 (:234-240) or z, theta (NMPC_TT.m:129-134)."""
+        return 2 if self.model == "uav5" else 5
+
+    @property
+    def np_min(self) -> int:
+        """length of [x0; xs]."""
+        return self.nx + 3
+
+    @property
     def m(self) -> int:
-        """g rows per stage: z, theta, x5, x6, x7 + one per obstacle (:234-244)."""
-        return 5 + self.n_obs
+        """g rows per stage: box rows + one per obstacle (:234-244)."""
+        return self.nb + self.n_obs
 
     @property
     def nw(self) -> int:
-        return NU * self.N
+        return self.nu * self.N
 
     @property
     def ng(self) -> int:
@@ -84,23 +102,24 @@ class ProblemSpec:
 
     @property
     def nX(self) -> int:
-        return NX * (self.N + 1)
+        return self.nx * (self.N + 1)
 
     def validate(self):
-        if self.model != "uav8g":
+        if self.model not in ("uav8g", "uav5"):
             raise ValueError(f"unsupported model {self.model!r}")
         if not (1 <= self.N <= 63):
             raise ValueError("N must be in [1, 63]")
         if self.n_obs > 16:
             raise ValueError("at most 16 obstacles")
-        if self.np < 11:
-            raise ValueError("np must be >= 11 (x0(8) + target(3))")
+        if self.np < self.np_min:
+            raise ValueError(f"np must be >= {self.np_min} (x0({self.nx}) + target(3))")
         for o in self.obstacles:
-            if o.x_pidx >= self.np or o.y_pidx >= self.np:
-                raise ValueError("obstacle parameter index out of range")
+            for i in (o.x_pidx, o.y_pidx):
+                if i != -1 and not (self.np_min <= i < self.np):
+                    raise ValueError("obstacle parameter index out of range")
         for i in (self.w1_pidx, self.w2_pidx):
-            if i != -1 and not (11 <= i < self.np):
-                raise ValueError("weight parameter index must be -1 or in [11, np)")
+            if i != -1 and not (self.np_min <= i < self.np):
+                raise ValueError("weight parameter index must be -1 or in [np_min, np)")
         if not self.T > 0:
             raise ValueError("T must be positive")
         return self
@@ -112,6 +131,12 @@ class ProblemSpec:
         ``lbg[0:240:15]``); here stride and length follow (N, n_obs)
         (SURVEY F3), so any N gives a feasible bound set.
         """
+        if self.model == "uav5":  # MATLAB/Dynamic Obstacles/NMPC_TT.m:140-149
+            lbx = np.tile([V_U_MIN, -OMEGA_2_U, -OMEGA_3_U], self.N)
+            ubx = np.tile([V_U_MAX, OMEGA_2_U, OMEGA_3_U], self.N)
+            lrow = np.concatenate([[Z_U_MIN, -THETA_U_MAX], np.full(self.n_obs, -np.inf)])
+            urow = np.concatenate([[Z_U_MAX, THETA_U_MAX], np.zeros(self.n_obs)])
+            return lbx, ubx, np.tile(lrow, self.N + 1), np.tile(urow, self.N + 1)
         lbx = np.tile([V_U_MIN, -OMEGA_2_U, -OMEGA_3_U, -OMEGA_G, -OMEGA_G, -OMEGA_G], self.N)
         ubx = np.tile([V_U_MAX, OMEGA_2_U, OMEGA_3_U, OMEGA_G, OMEGA_G, OMEGA_G], self.N)
         lrow = np.concatenate([[Z_U_MIN, -THETA_U_MAX, -PHI_G_MAX, -THETA_G_MAX, -SHI_G_MAX],
@@ -122,7 +147,8 @@ class ProblemSpec:
 
 
 def make_spec(layout: str | None = "nmpc_tt", N: int = 15, T: float = 1.0, dynamic: bool = False,
-              obstacles: Sequence[Obstacle] | None = None, weights_in_p: bool = False) -> ProblemSpec:
+              obstacles: Sequence[Obstacle] | None = None, weights_in_p: bool = False,
+              model: str = "uav8g") -> ProblemSpec:
     """Spec for a reference scenario family.
 
     layout: one of LAYOUTS (None = no obstacles).  dynamic=True makes the y
@@ -130,26 +156,31 @@ def make_spec(layout: str | None = "nmpc_tt", N: int = 15, T: float = 1.0, dynam
     Dynamic Obstacle avoidance.m:52,128-133), np = 17.  weights_in_p=True
     appends the cost weights (w1, w2) to p, one pair per scenario: the batched
     form of the RL replay that rebuilds nlpsol per weight pair
-    (MATLAB/Race Track 1/MPC.m:1,127).
+    (MATLAB/Race Track 1/MPC.m:1,127).  model="uav5" is the
+    no-gimbal variant (MATLAB/Dynamic Obstacles/NMPC_TT.m): p = [x0(5); xs(3); ...].
     """
+    np0 = 8 if model == "uav5" else 11
     if obstacles is None:
         obstacles = ()
         if layout is not None:
             xy, r = LAYOUTS[layout]
             obstacles = tuple(
-                Obstacle(float(x), float(y), UAV_R + r, -1, (11 + j) if (dynamic and j < 6) else -1)
+                Obstacle(float(x), float(y), UAV_R + r, -1, (np0 + j) if (dynamic and j < 6) else -1)
                 for j, (x, y) in enumerate(xy))
-    npar = 17 if dynamic else 11
+    npar = np0 + 6 if dynamic else np0
     w1p = w2p = -1
     if weights_in_p:
         w1p, w2p, npar = npar, npar + 1, npar + 2
-    return ProblemSpec(N=N, T=T, obstacles=tuple(obstacles), np=npar, w1_pidx=w1p, w2_pidx=w2p).validate()
+    return ProblemSpec(N=N, T=T, obstacles=tuple(obstacles), np=npar, w1_pidx=w1p, w2_pidx=w2p,
+                       model=model).validate()
 
 
 # SURVEY.md section 8 configurations
 def config_spec(cfg: int) -> ProblemSpec:
-    if cfg == 1:   # NMPC_TT.py as written (N=15, T=1, 3 obstacles)
+    if cfg == 0:   # Python/NMPC_TT.py as written (N=15, T=1, 3 obstacles)
         return make_spec("nmpc_tt", N=15, T=1.0)
+    if cfg == 1:   # plumbing: no-gimbal model, N=10, 0 obstacles (BASELINE configs[0], SURVEY F6)
+        return make_spec(None, N=10, T=0.2, model="uav5")
     if cfg == 2:   # batch 1024, N=20, 0 obstacles, T=0.2
         return make_spec(None, N=20, T=0.2)
     if cfg in (3, 4):  # N=20, 10 active obstacles (Race Track 2.py), T=0.2

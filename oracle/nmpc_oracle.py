@@ -104,9 +104,32 @@ class Problem:
     # cost weights taken from p (batched weight sweep): index or -1
     w1_pidx: int = -1
     w2_pidx: int = -1
+    # "uav8g": 8 states / 6 controls (Python/NMPC_TT.py:94-151);
+    # "uav5": no gimbal, 5 states / 3 controls, distance cost, rows [z, theta]
+    # (MATLAB/Dynamic Obstacles/NMPC_TT.m:26-35,102-111,129-134)
+    model: str = "uav8g"
 
-    nx = 8
-    nu = 6
+    @property
+    def nx(self):
+        return 5 if self.model == "uav5" else 8
+
+    @property
+    def nu(self):
+        return 3 if self.model == "uav5" else 6
+
+    @property
+    def box_states(self):
+        """state index of each box row of a stage (z, theta, x5, x6, x7 / z, theta)."""
+        return [2, 3] if self.model == "uav5" else [2, 3, 5, 6, 7]
+
+    @property
+    def nb(self):
+        return len(self.box_states)
+
+    @property
+    def target_index(self):
+        """index of the target's x in p (P(6) in the no-gimbal script, P(9) else)."""
+        return self.nx
 
     def __post_init__(self):
         self.obs_x = np.asarray(self.obs_x, dtype=float)
@@ -126,7 +149,7 @@ class Problem:
 
     @property
     def m(self):
-        return 5 + self.n_obs
+        return self.nb + self.n_obs
 
     @property
     def nw(self):
@@ -156,30 +179,44 @@ class Problem:
         return ox, oy
 
 
-def make_problem(layout: str | None, N: int, T: float, dynamic: bool = False) -> Problem:
+def make_problem(layout: str | None, N: int, T: float, dynamic: bool = False, model: str = "uav8g") -> Problem:
     """Problem for a named reference obstacle layout (None = 0 obstacles)."""
+    np0 = 8 if model == "uav5" else 11
     if layout is None:
-        return Problem(N=N, T=T)
+        return Problem(N=N, T=T, model=model, np_=np0)
     xy, r = OBSTACLE_LAYOUTS[layout]
     ox = np.array([a for a, _ in xy], float)
     oy = np.array([b for _, b in xy], float)
     rs = np.full(len(xy), UAV_R + r)
     ypidx = -np.ones(len(xy), dtype=int)
-    np_ = 11
+    np_ = np0
     if dynamic:
-        ypidx[:6] = np.arange(11, 17)  # P(12:17) in MATLAB 1-based
-        np_ = 17
-    return Problem(N=N, T=T, obs_x=ox, obs_y=oy, obs_rsum=rs, obs_y_pidx=ypidx, np_=np_)
+        ypidx[:6] = np.arange(np0, np0 + 6)  # P(12:17) in MATLAB 1-based
+        np_ = np0 + 6
+    return Problem(N=N, T=T, obs_x=ox, obs_y=oy, obs_rsum=rs, obs_y_pidx=ypidx, np_=np_, model=model)
 
 
-# --- bounds: Python/NMPC_TT.py:269-306, generalised (stride m, N+1 stages) ---
 def bounds(prob: Problem):
-    N, m = prob.N, prob.m
+    N = prob.N
+    if prob.model == "uav5":  # MATLAB/Dynamic Obstacles/NMPC_TT.m:140-149
+        lbx = np.tile([V_MIN, -W2U, -W3U], N)
+        ubx = np.tile([V_MAX, W2U, W3U], N)
+        lrow = np.concatenate([[Z_MIN, -THETA_U], np.full(prob.n_obs, -np.inf)])
+        urow = np.concatenate([[Z_MAX, THETA_U], np.zeros(prob.n_obs)])
+        return lbx, ubx, np.tile(lrow, N + 1), np.tile(urow, N + 1)
     lbx = np.tile([V_MIN, -W2U, -W3U, -WG, -WG, -WG], N)
     ubx = np.tile([V_MAX, W2U, W3U, WG, WG, WG], N)
     lrow = np.concatenate([[Z_MIN, -THETA_U, -PHI_G, -THETA_G, -SHI_G], np.full(prob.n_obs, -np.inf)])
     urow = np.concatenate([[Z_MAX, THETA_U, PHI_G, THETA_G, SHI_G], np.zeros(prob.n_obs)])
     return lbx, ubx, np.tile(lrow, N + 1), np.tile(urow, N + 1)
+
+
+def _pad8(x):
+    """no-gimbal state / control padded into the gimbal model's (the no-gimbal
+    dynamics are its first five components, MATLAB/Dynamic Obstacles/NMPC_TT.m:37-38)."""
+    out = np.zeros(8 if len(x) == 5 else 6)
+    out[:len(x)] = x
+    return out
 
 
 # --- model: Python/NMPC_TT.py:139-148 ----------------------------------------
@@ -194,17 +231,28 @@ def unpack_w(prob, w):
     return np.asarray(w, float).reshape(prob.N, prob.nu).T
 
 
+def dynamics5(x, u):
+    """No-gimbal kinematics, MATLAB/Dynamic Obstacles/NMPC_TT.m:37-38."""
+    th, ps, v = x[3], x[4], u[0]
+    return np.array([v * math.cos(ps) * math.cos(th), v * math.sin(ps) * math.cos(th),
+                     v * math.sin(th), u[1], u[2]])
+
+
 def rollout(prob, U, x0):
-    """X[:,0] = P[0:8]; X[:,k+1] = X[:,k] + T f(X[:,k], U[:,k])  (:160-167)."""
-    X = np.zeros((8, prob.N + 1))
+    """X[:,0] = P[0:nx]; X[:,k+1] = X[:,k] + T f(X[:,k], U[:,k])  (:160-167; NMPC_TT.m:49-54)."""
+    f = dynamics5 if prob.model == "uav5" else dynamics
+    X = np.zeros((prob.nx, prob.N + 1))
     X[:, 0] = x0
     for k in range(prob.N):
-        X[:, k + 1] = X[:, k] + prob.T * dynamics(X[:, k], U[:, k])
+        X[:, k + 1] = X[:, k] + prob.T * f(X[:, k], U[:, k])
     return X
 
 
 def stage_cost(prob, xk, xt, yt):
-    """Literal restatement of Python/NMPC_TT.py:209-220 for one stage."""
+    """Literal restatement of Python/NMPC_TT.py:209-220 for one stage (no-gimbal
+    model: the distance term only, MATLAB/Dynamic Obstacles/NMPC_TT.m:102-105)."""
+    if prob.model == "uav5":
+        return prob.w1 * math.sqrt((xk[0] - xt) ** 2 + (xk[1] - yt) ** 2)
     hv, hh = prob.vfov / 2, prob.hfov / 2
     z = xk[2]
     a = (z * math.tan(xk[6] + hv) - z * math.tan(xk[6] - hv)) / 2
@@ -222,17 +270,18 @@ def stage_cost(prob, xk, xt, yt):
 def stage_rows(prob, xk, ox, oy):
     """g rows for one stage (Python/NMPC_TT.py:234-244)."""
     d = np.sqrt((xk[0] - ox) ** 2 + (xk[1] - oy) ** 2)
-    return np.concatenate([[xk[2], xk[3], xk[5], xk[6], xk[7]], -d + prob.obs_rsum])
+    return np.concatenate([xk[prob.box_states], -d + prob.obs_rsum])
 
 
 def objective(prob, w, p):
     prob = prob.weighted(p)
-    X = rollout(prob, unpack_w(prob, w), p[:8])
-    return sum(stage_cost(prob, X[:, k], p[8], p[9]) for k in range(prob.N))
+    X = rollout(prob, unpack_w(prob, w), p[:prob.nx])
+    ti = prob.target_index
+    return sum(stage_cost(prob, X[:, k], p[ti], p[ti + 1]) for k in range(prob.N))
 
 
 def constraints(prob, w, p):
-    X = rollout(prob, unpack_w(prob, w), p[:8])
+    X = rollout(prob, unpack_w(prob, w), p[:prob.nx])
     ox, oy = prob.obstacles(p)
     return np.concatenate([stage_rows(prob, X[:, k], ox, oy) for k in range(prob.N + 1)])
 
@@ -241,7 +290,20 @@ def constraints(prob, w, p):
 _V = [0, 1, 2, 5, 6, 7]  # state indices the stage cost depends on
 
 
+def _as8(prob):
+    """the gimbal-model problem whose first 5 states / 3 controls are the no-gimbal model's."""
+    import dataclasses
+    return dataclasses.replace(prob, model="uav8g", w2=0.0)
+
+
 def stage_cost_derivs(prob, xk, xt, yt):
+    if prob.model == "uav5":
+        v, g, H = stage_cost_derivs(_as8(prob), _pad8(xk), xt, yt)
+        return v, g[:5], H[:5, :5]
+    return _stage_cost_derivs8(prob, xk, xt, yt)
+
+
+def _stage_cost_derivs8(prob, xk, xt, yt):
     """(value, grad (8,), hess (8,8)) of the stage cost of :209-220.
 
     Uses the algebraically equal form  Q = A ex^2 + B ex ey + C ey^2
@@ -328,6 +390,9 @@ def obstacle_derivs(xk, ox, oy):
 
 def dyn_jac(prob, xk, uk):
     """A = I + T f_x, B = T f_u for the Euler step (:162-167)."""
+    if prob.model == "uav5":
+        A, B = dyn_jac(_as8(prob), _pad8(xk), _pad8(uk))
+        return A[:5, :5], B[:5, :3]
     T = prob.T
     th, ps, v = xk[3], xk[4], uk[0]
     ct, st, cp, sp = math.cos(th), math.sin(th), math.cos(ps), math.sin(ps)
@@ -344,6 +409,9 @@ def dyn_jac(prob, xk, uk):
 
 def dyn_hess(prob, xk, uk, lam):
     """Second derivatives of lam^T (T f(x,u)): (Hxx (8,8), Hxu (8,6))."""
+    if prob.model == "uav5":
+        Hxx, Hxu = dyn_hess(_as8(prob), _pad8(xk), _pad8(uk), _pad8(lam))
+        return Hxx[:5, :5], Hxu[:5, :3]
     T = prob.T
     th, ps, v = xk[3], xk[4], uk[0]
     ct, st, cp, sp = math.cos(th), math.sin(th), math.cos(ps), math.sin(ps)
@@ -371,36 +439,37 @@ class SSEval:
         self.prob = prob
         N, nw = prob.N, prob.nw
         self.p = np.asarray(p, float)
+        nx, nu = prob.nx, prob.nu
         self.U = unpack_w(prob, w)
-        self.X = rollout(prob, self.U, self.p[:8])
+        self.X = rollout(prob, self.U, self.p[:nx])
         self.ox, self.oy = prob.obstacles(self.p)
-        xt, yt = self.p[8], self.p[9]
+        xt, yt = self.p[prob.target_index], self.p[prob.target_index + 1]
         self.F = 0.0
-        self.gl = np.zeros((N + 1, 8))
-        self.Hl = np.zeros((N + 1, 8, 8))
+        self.gl = np.zeros((N + 1, nx))
+        self.Hl = np.zeros((N + 1, nx, nx))
         for k in range(N):
             v, g, H = stage_cost_derivs(prob, self.X[:, k], xt, yt)
             self.F += v
             self.gl[k], self.Hl[k] = g, H
         self.g = np.concatenate([stage_rows(prob, self.X[:, k], self.ox, self.oy) for k in range(N + 1)])
         # dynamics jacobians and forward sensitivities Z_k = dX_k/dw
-        self.A = np.zeros((N, 8, 8))
-        self.B = np.zeros((N, 8, 6))
-        self.Z = np.zeros((N + 1, 8, nw))
+        self.A = np.zeros((N, nx, nx))
+        self.B = np.zeros((N, nx, nu))
+        self.Z = np.zeros((N + 1, nx, nw))
         for k in range(N):
             self.A[k], self.B[k] = dyn_jac(prob, self.X[:, k], self.U[:, k])
             self.Z[k + 1] = self.A[k] @ self.Z[k]
-            self.Z[k + 1][:, 6 * k:6 * k + 6] += self.B[k]
+            self.Z[k + 1][:, nu * k:nu * k + nu] += self.B[k]
         # constraint-row jacobians wrt X_k
         m = prob.m
-        self.Gk = np.zeros((N + 1, m, 8))
+        self.Gk = np.zeros((N + 1, m, nx))
         self.Hg = np.zeros((N + 1, prob.n_obs, 2, 2))
         for k in range(N + 1):
-            for i, idx in enumerate([2, 3, 5, 6, 7]):
+            for i, idx in enumerate(prob.box_states):
                 self.Gk[k, i, idx] = 1.0
             if prob.n_obs:
                 G2, H2 = obstacle_derivs(self.X[:, k], self.ox, self.oy)
-                self.Gk[k, 5:, 0:2] = G2
+                self.Gk[k, prob.nb:, 0:2] = G2
                 self.Hg[k] = H2
         # stage 0 is constant in w (X_0 = p[0:8], F7): Z_0 = 0, so its terms are
         # structurally absent -- as in CasADi's symbolic AD -- and are skipped
@@ -413,7 +482,8 @@ class SSEval:
         N, m, nw = prob.N, prob.m, prob.nw
         lam = np.asarray(lam_g, float).reshape(N + 1, m)
         # adjoint: lam_k = obj*gl_k + G_k^T y_k + A_k^T lam_{k+1}
-        adj = np.zeros((N + 2, 8))
+        nx, nu, nb = prob.nx, prob.nu, prob.nb
+        adj = np.zeros((N + 2, nx))
         for k in range(N, 0, -1):
             adj[k] = obj_factor * self.gl[k] + self.Gk[k].T @ lam[k]
             if k < N:
@@ -422,17 +492,17 @@ class SSEval:
         for k in range(1, N + 1):
             Hxx = obj_factor * self.Hl[k]
             if prob.n_obs:
-                Hxx[0:2, 0:2] += np.einsum("j,jab->ab", lam[k, 5:], self.Hg[k])
-            Hxu = np.zeros((8, 6))
+                Hxx[0:2, 0:2] += np.einsum("j,jab->ab", lam[k, nb:], self.Hg[k])
+            Hxu = np.zeros((nx, nu))
             if k < N:
                 dHxx, Hxu = dyn_hess(prob, self.X[:, k], self.U[:, k], adj[k + 1])
                 Hxx = Hxx + dHxx
             Zk = self.Z[k]
             W += Zk.T @ Hxx @ Zk
             if k < N:
-                C = Zk.T @ Hxu  # (nw, 6)
-                W[:, 6 * k:6 * k + 6] += C
-                W[6 * k:6 * k + 6, :] += C.T
+                C = Zk.T @ Hxu  # (nw, nu)
+                W[:, nu * k:nu * k + nu] += C
+                W[nu * k:nu * k + nu, :] += C.T
         return W
 
 
@@ -1374,7 +1444,8 @@ def cviol_unscaled(d, dc, gl_, gu_, slm, sum_):
 def shift_timestep(prob, x0, u, xs, con_t=(12.0, 0.01)):
     """Plant Euler step with u[:,0], warm start shift, target unicycle step."""
     T = prob.T
-    x0n = x0 + T * dynamics(x0, u[:, 0])
+    f = dynamics5 if prob.model == "uav5" else dynamics
+    x0n = x0 + T * f(x0, u[:, 0])
     u0 = np.concatenate([u[:, 1:], u[:, -1:]], axis=1)
     v, w = con_t
     xsn = xs + T * np.array([v * math.cos(xs[2]), v * math.sin(xs[2]), w])

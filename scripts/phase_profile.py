@@ -6,7 +6,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "mpc-implementation_amd"))
 from nmpc_amd import nlpsol, config_spec, draw_scenarios, REFERENCE_OPTS
 PH = ["rollout", "eval", "derivs", "adjoint", "summaries", "riccati", "resolve", "forward", "row_step",
-      "barrier", "ftb", "dual_ftb", "conv+mu", "accept", "init", "TOTAL", "ric.1", "#factor", "#soc", "ric.2", "ric.3"]
+      "barrier", "ftb", "dual_ftb", "conv+mu", "accept", "init", "TOTAL", "ric.1", "#factor", "#soc", "ric.2", "ric.3", "sigx", "ls_setup", "filter"]
 cfg = int(sys.argv[1]) if len(sys.argv) > 1 else 3
 B = int(sys.argv[2]) if len(sys.argv) > 2 else 4096
 spec = config_spec(cfg)
@@ -25,8 +25,8 @@ tot = st[:, 15].mean()
 print(f"B={B} mean iters {np.mean(it):.2f}; mean total cycles/scenario {tot:.3e} ({tot/np.mean(it):.3e} per iter)")
 for i, n in enumerate(PH[:15]):
     print(f"  {n:10s} {st[:, i].mean():12.4e}  {100*st[:, i].mean()/tot:6.2f}%  per-iter {st[:, i].mean()/np.mean(it):10.1f}")
-print(f"  unattributed {100*(tot - st[:, :15].sum(1).mean())/tot:6.2f}%")
-for i in range(16, 21):
+print(f"  unattributed {100*(tot - st[:, :15].sum(1).mean() - st[:, 21:24].sum(1).mean())/tot:6.2f}%")
+for i in range(16, 24):
     print(f"  {PH[i]:10s} {st[:, i].mean():12.4e}  {100*st[:, i].mean()/tot:6.2f}%  per-iter {st[:, i].mean()/np.mean(it):10.1f}")
 tot_c = st[:, 15]
 print("per-scenario total cycles: p50 %.3e p90 %.3e p99 %.3e max %.3e" % tuple(np.percentile(tot_c, [50, 90, 99, 100])))

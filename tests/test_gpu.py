@@ -481,3 +481,44 @@ def test_closed_loop_moving_obstacles_match_oracle_loop():
             x1, u1, xs1 = orc.shift_timestep(prob, pk[:8], r["x"].reshape(spec.N, 6).T, pk[8:11])
             pk = np.concatenate([x1, xs1, pk[11:] + dp[k, 11:]])
             u0 = u1.T.ravel()
+
+
+@pytest.mark.parametrize("layout,N,seed", [(None, 10, 1001), ("10_obstacles", 15, 77)])
+def test_no_gimbal_model_parity(layout, N, seed):
+    """No-gimbal variant (MATLAB/Dynamic Obstacles/NMPC_TT.m) run on the
+    gimbal kernel with the gimbal controls/states absent, against the oracle's
+    dense IPOPT on the true 3N-variable problem."""
+    from nmpc_amd import make_spec, draw_scenarios
+
+    spec = make_spec(layout, N=N, T=0.2, model="uav5")
+    assert (spec.nw, spec.m, spec.np) == (3 * N, 2 + spec.n_obs, 8)
+    B = 4
+    P = draw_scenarios(spec, B, seed=seed)
+    lbx, ubx, lbg, ubg = spec.bounds()
+    s = _solver(spec)
+    sol = s(x0=np.zeros(spec.nw), lbx=lbx, ubx=ubx, lbg=lbg, ubg=ubg, p=P.T)
+    assert sol["x"].shape == (3 * N, B) and sol["X"].shape == (5 * (N + 1), B)
+    st, its = s.stats()["status_code"], s.stats()["iter_count"]
+    prob = orc.make_problem(layout, N=N, T=0.2, model="uav5")
+    ref = orc.IpoptDense(prob, orc.REFERENCE_OPTS)
+    for b in range(B):
+        r = ref.solve(np.zeros(spec.nw), lbx, ubx, lbg, ubg, P[b])
+        assert int(st[b]) == r["status"], (b, st[b], r["status"])
+        assert abs(int(its[b]) - r["iter"]) <= 2
+        if r["status"] == 0:
+            assert _rel(sol["x"][:, b], r["x"]) <= TOL
+            assert _rel(sol["X"][:, b], r["X"].T.ravel()) <= TOL
+            assert abs(sol["f"][0, b] - r["f"]) <= TOL * (1 + abs(r["f"]))
+
+
+def test_no_gimbal_model_entry_points():
+    from nmpc_amd import make_spec, _lib
+    import torch
+
+    spec = make_spec(None, N=10, T=0.2, model="uav5")
+    s = _solver(spec)
+    f64 = dict(dtype=torch.float64, device="cuda")
+    B = 2
+    with pytest.raises(_lib.NmpcError):
+        s.shift_device(torch.zeros(B, spec.np, **f64), torch.zeros(B, spec.nw, **f64),
+                       torch.zeros(B, spec.nw, **f64), torch.zeros(B, **f64), torch.zeros(B, **f64))

@@ -147,3 +147,45 @@ def test_closed_loop_shift_matches_reference_formula():
     np.testing.assert_allclose(x1[3:5], [0.01, 0.02])
     assert u1[0, 0] == 21.0 and u1[0, 2] == 20.0
     np.testing.assert_allclose(xs1, [112.0, 150.0, 0.01])
+
+
+def test_no_gimbal_model_functions_and_bounds():
+    """No-gimbal variant (MATLAB/Dynamic Obstacles/NMPC_TT.m): 5-state kinematics
+    (:37-38), distance cost (:102-105), rows [z, theta] (:129-134) and the
+    script's literal N=15 bound vectors (:140-149)."""
+    import math
+    prob5 = orc.make_problem(None, N=15, T=0.2, model="uav5")
+    lbx, ubx, lbg, ubg = orc.bounds(prob5)
+    assert len(lbx) == 45 and len(lbg) == 32
+    np.testing.assert_array_equal(lbg[0::2], 75.0)
+    np.testing.assert_array_equal(ubg[0::2], 150.0)
+    np.testing.assert_array_equal(lbg[1::2], -0.2618)
+    np.testing.assert_array_equal(ubg[1::2], 0.2618)
+    np.testing.assert_array_equal(lbx[0::3], 14.0)
+    np.testing.assert_array_equal(ubx[1::3], math.pi / 30)
+    np.testing.assert_array_equal(ubx[2::3], math.pi / 21)
+    rng = np.random.default_rng(3)
+    w5 = rng.uniform(lbx, ubx)
+    p5 = np.array([90.0, 150.0, 80.0, 0.05, 0.3, 100.0, 150.0, 0.0])
+    # literal restatement of the MATLAB rollout / objective / g
+    X = np.zeros((5, 16))
+    X[:, 0] = p5[:5]
+    U = w5.reshape(15, 3).T
+    F = 0.0
+    for k in range(15):
+        th, ps, v = X[3, k], X[4, k], U[0, k]
+        X[:, k + 1] = X[:, k] + 0.2 * np.array([v * math.cos(ps) * math.cos(th), v * math.sin(ps) * math.cos(th),
+                                                v * math.sin(th), U[1, k], U[2, k]])
+        F += math.sqrt((X[0, k] - p5[5]) ** 2 + (X[1, k] - p5[6]) ** 2)
+    assert abs(orc.objective(prob5, w5, p5) - F) <= 1e-12 * F
+    np.testing.assert_allclose(orc.constraints(prob5, w5, p5), X[2:4].T.ravel(), rtol=1e-14)
+    # derivatives: finite differences of the literal functions
+    ev = orc.SSEval(prob5, w5, p5)
+    h = 1e-6
+    for j in (0, 7, 20, 44):
+        e = np.zeros(45)
+        e[j] = h
+        fd = (orc.objective(prob5, w5 + e, p5) - orc.objective(prob5, w5 - e, p5)) / (2 * h)
+        assert abs(ev.gradF[j] - fd) <= 1e-6 * (1 + abs(fd))
+        fdg = (orc.constraints(prob5, w5 + e, p5) - orc.constraints(prob5, w5 - e, p5)) / (2 * h)
+        np.testing.assert_allclose(ev.J[:, j], fdg, atol=1e-6)
