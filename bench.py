@@ -130,6 +130,8 @@ def main():
                          "per_step: one solve launch + shift launch per step; cold: per step, u=0 each step")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-per-step", action="store_true", help="skip the per-step-launch comparison line")
+    ap.add_argument("--in-order", action="store_true",
+                    help="fused mode: dispatch scenarios in index order (no longest-first order)")
     ap.add_argument("--cpu-budget", type=float, default=15.0)
     args = ap.parse_args()
 
@@ -137,6 +139,7 @@ def main():
     import torch.distributed as dist
     from nmpc_amd import nlpsol, config_spec, draw_scenarios, REFERENCE_OPTS
     from nmpc_amd.dist import shard, pack_result, gather_rows
+    from nmpc_amd.schedule import longest_first
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -204,10 +207,10 @@ def main():
         hist["u"][k].copy_(out["x"][:, :6]); hist["f"][k].copy_(out["f"])
         hist["iters"][k].copy_(out["iters"]); hist["status"][k].copy_(out["status"])
 
-    def fused(p, w, hist, k_steps, timed_events=None):
+    def fused(p, w, hist, k_steps, timed_events=None, order=None):
         if timed_events is not None:
             timed_events[0].record(stream)
-        solver.closed_loop_device(k_steps, *bnd, p, w, v_t, w_t, hist, stream=stream)
+        solver.closed_loop_device(k_steps, *bnd, p, w, v_t, w_t, hist, stream=stream, order=order)
         if timed_events is not None:
             timed_events[1].record(stream)
         if world > 1:  # the only exchange: final gather of every step's (u0, f, status)
@@ -226,16 +229,21 @@ def main():
         # warmup: W MPC steps advance the closed loop (one solve + shift launch per step)
         for k in range(W):
             per_step(p, w, hw, k, mode == "cold")
+        order = None
+        if mode == "fused" and W > 0 and not args.in_order:
+            # longest-expected-first dispatch from the iterations of the W warm-up
+            # steps, which precede the timed steps (nmpc_amd.schedule)
+            order = longest_first(hw["iters"][:W])
         if mode == "fused":
             # the timed launch once on scratch copies of the same state (code objects,
             # workspace): the fused kernel then runs exactly twice with identical work
-            fused(p.clone(), w.clone(), hist_bufs(K), K)
+            fused(p.clone(), w.clone(), hist_bufs(K), K, order=order)
         barrier_sync()
         evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
                for _ in range(1 if mode == "fused" else K)]
         t0 = time.perf_counter()
         if mode == "fused":
-            fused(p, w, ht, K, evs[0])
+            fused(p, w, ht, K, evs[0], order=order)
         else:
             for k in range(K):
                 per_step(p, w, ht, k, mode == "cold", evs[k])
@@ -301,6 +309,10 @@ def main():
             "mean_ip_iterations": ibar,
             "status_histogram": status_hist,
         }
+        if args.mode == "fused":
+            res["dispatch"] = ("index order" if (args.in_order or W == 0) else
+                               "longest-expected-first: scenarios sorted by the iterations of the "
+                               f"{W} warm-up MPC steps that precede the timed steps (nmpc_amd.schedule)")
         if fov_mean is not None:
             res["closed_loop_fov_error_mean_m"] = fov_mean  # Python/NMPC_TT.py:433-437 metric, per step
         if side is not None:

@@ -184,7 +184,13 @@ int nmpc_shift_dev(nmpc_handle* h, int32_t B, double* p, int64_t ld_p,
  *   p   : np x B (ld_p >= np), in/out (advanced K steps)
  *   w   : nw x B (ld nw), in: first warm start; out: the last step's shifted solution
  *   u_hist K x B x 6, x_hist K x B x 8, f_hist / fov_hist / status_hist /
- *   iters_hist K x B; each nullable.  Bounds as in nmpc_solve_batch_dev. */
+ *   iters_hist K x B; each nullable.  Bounds as in nmpc_solve_batch_dev.
+ *   order: nullable, B int32 (device): a permutation of 0..B-1 giving the order in
+ *          which scenarios are dispatched to wavefronts (order[g] runs g-th).  Results
+ *          do not depend on it.  Putting the longest expected chains first (e.g.
+ *          sorted by the previous launch's iterations, nmpc_amd.schedule) keeps a
+ *          long chain from starting after the first wave of slots has drained.
+ *          Entries outside [0,B) are skipped; duplicates are the caller's error. */
 int nmpc_closed_loop_dev(nmpc_handle* h, int32_t B, int32_t K,
                          const double* lbx, int64_t ld_lbx, const double* ubx, int64_t ld_ubx,
                          const double* lbg, int64_t ld_lbg, const double* ubg, int64_t ld_ubg,
@@ -192,7 +198,7 @@ int nmpc_closed_loop_dev(nmpc_handle* h, int32_t B, int32_t K,
                          const double* v_t, const double* w_t, int64_t ld_tk, int64_t ld_tb,
                          const double* p_step, int64_t ld_ps,
                          double* u_hist, double* x_hist, double* f_hist, double* fov_hist,
-                         int32_t* status_hist, int32_t* iters_hist, void* stream);
+                         int32_t* status_hist, int32_t* iters_hist, const int32_t* order, void* stream);
 
 const char* nmpc_last_error(void);
 

@@ -784,9 +784,23 @@ struct Solver {
     while (tR >= 0 && (rR + 1) * (rR + 2) / 2 <= tR) ++rR;
     const int cR = tR >= 0 ? tR - rR * (rR + 1) / 2 : 0;
     const int rowS = (i >= 1 && i < 6) ? 2 + i : 3;
+    // stage operands in global memory (Q_k entry, diag R_k entry, r_k) do not depend on
+    // the recursion: fetch stage k-1's while stage k is formed, so the sweep never
+    // waits on a global load.  Lanes 0..5 hold r_k (broadcast by readlane).
+    const bool diagR = tR >= 0 && rR == cR;
+    const int lr = lanef() < 6 ? lanef() : 5;
+    double qvn = Qs[(N - 1) * 36 + ij];
+    double rdn = (diagR && Rd) ? Rd[(N - 1) * 6 + rR] : 1.0;
+    double rvn = rv[(N - 1) * 6 + lr];
     sync();
     bool ok = true;
     for (int k = N - 1; k >= 0; --k) {
+      const double qv = qvn, rdk = rdn, rvk = rvn;
+      if (k > 0) {
+        qvn = Qs[(k - 1) * 36 + ij];
+        if (diagR && Rd) rdn = Rd[(k - 1) * 6 + rR];
+        rvn = rv[(k - 1) * 6 + lr];
+      }
       double E03, E04, E13, E14, E23, b00, b10, b20;
       stage_AB(k, E03, E04, E13, E14, E23, b00, b10, b20);
       const double aj0 = (j == 3) ? E03 : (j == 4 ? E04 : 0.0);
@@ -795,7 +809,6 @@ struct Solver {
       const double ai0 = (i == 3) ? E03 : (i == 4 ? E04 : 0.0);
       const double ai1 = (i == 3) ? E13 : (i == 4 ? E14 : 0.0);
       const double ai2 = (i == 3) ? E23 : 0.0;
-      const double qv = Qs[k * 36 + ij];  // global, issued early
       double APA;
       // ---- (1)
       { STAMP0();
@@ -824,7 +837,7 @@ struct Solver {
             v = T * (T * Pc[(2 + rR) * 8 + 2 + cR]);
           }
           // an absent control (model embedding) keeps a unit pivot: zero step, no inertia effect
-          if (rR == cR) v = (rR >= nuE) ? 1.0 : v + ((Rd ? Rd[k * 6 + rR] : 1.0) + delta);
+          if (rR == cR) v = (rR >= nuE) ? 1.0 : v + (rdk + delta);
           Rc[tR] = v;
           Rk[k * 21 + tR] = v;
         }
@@ -853,9 +866,9 @@ struct Solver {
             Lm[r * (r + 1) / 2 + c] = v * ig;
           }
         }
-        rt[0] = rv[k * 6 + 0] + ((b00 * pc[0] + b10 * pc[1]) + b20 * pc[2]);
+        rt[0] = readlane_d(rvk, 0) + ((b00 * pc[0] + b10 * pc[1]) + b20 * pc[2]);
 #pragma unroll
-        for (int r = 1; r < 6; ++r) rt[r] = rv[k * 6 + r] + T * pc[2 + r];
+        for (int r = 1; r < 6; ++r) rt[r] = readlane_d(rvk, r) + T * pc[2 + r];
         if (lanef() < 9) {
           // column lanef() of K = -R~^{-1} S~ (lane 8: k = -R~^{-1} r~) by two
           // triangular solves with the Cholesky factor
@@ -1828,7 +1841,7 @@ __device__ __forceinline__ void resto_phase(const Params* __restrict__ prm, doub
 
 // One scenario's solve (the whole IPOPT loop) by the calling wavefront.
 template <class CAP>
-__device__ __forceinline__ void solve_one(Solver<CAP>& S, const Params* __restrict__ prm, const IO& io, const int b) {
+__device__ __forceinline__ int solve_one(Solver<CAP>& S, const Params* __restrict__ prm, const IO& io, const int b) {
   auto lanef = [&]() { return S.lanef(); };  // for the STAMP macros
   (void)lanef;
   LDS double* stamps = S.stamps;
@@ -2456,6 +2469,9 @@ __device__ __forceinline__ void solve_one(Solver<CAP>& S, const Params* __restri
       }
     }
     ++it;
+#ifdef NMPC_PRIO
+    if (it == NMPC_PRIO) __builtin_amdgcn_s_setprio(3);
+#endif
     if (trace && S.lanef() == 0) {
       double th = 0.0;
       for (int r = 0; r < ng; ++r) th += fabs(S.d[r] - S.s[r]);
@@ -2517,6 +2533,7 @@ __device__ __forceinline__ void solve_one(Solver<CAP>& S, const Params* __restri
     if (io.status) io.status[b] = status;
     if (io.iters) io.iters[b] = it;
   }
+  return it;
 }
 
 template <class CAP>
@@ -2544,19 +2561,25 @@ struct Loop {
   const double* pstep;               // K x np parameter increments after each step (nullable)
   long long ld_ps;
   int *st_hist, *it_hist;            // K x B (nullable)
+  const int* order;                  // dispatch order: workgroup g runs scenario order[g] (nullable)
 };
 
 template <class CAP>
 __global__ __launch_bounds__(WAVE, NMPC_WAVES_PER_EU) void nmpc_closed_loop_kernel(const Params* __restrict__ prm, int B, IO io,
                                                                     Loop lp) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
-  const int b = blockIdx.x;
-  if (b >= B) return;
+  // longest-expected-first dispatch: workgroups start roughly in blockIdx order, so a
+  // caller-supplied permutation puts the longest closed-loop chains on the first wave
+  // of slots (an out-of-range entry is skipped, never dereferenced)
+  const int b = lp.order ? lp.order[blockIdx.x] : (int)blockIdx.x;
+  if (b < 0 || b >= B) return;
   const int nw = prm->nw;
   const double T = prm->T;
   double* wb = lp.w + (long long)b * nw;
   double* pb = lp.p + (long long)b * lp.ld_p;
   constexpr int WR = (6 * CAP::nmax + WAVE - 1) / WAVE;
+  int cum_it = 0;
+  (void)cum_it;
   for (int k = 0; k < lp.K; ++k) {
     // a fresh solver per step: no member is live across steps (a solver kept
     // outside the loop costs ~40 VGPRs of spills)
@@ -2569,7 +2592,14 @@ __global__ __launch_bounds__(WAVE, NMPC_WAVES_PER_EU) void nmpc_closed_loop_kern
     ik.f_out = lp.f_hist ? lp.f_hist + kb : nullptr;
     ik.status = lp.st_hist ? lp.st_hist + kb : nullptr;
     ik.iters = lp.it_hist ? lp.it_hist + kb : nullptr;
-    solve_one<CAP>(S, prm, ik, b);
+    const int its = solve_one<CAP>(S, prm, ik, b);
+#ifdef NMPC_PRIO
+    cum_it += its;
+    if (cum_it > 30 * (k + 1)) __builtin_amdgcn_s_setprio(2);
+    else __builtin_amdgcn_s_setprio(0);
+#else
+    (void)its;
+#endif
     sync();
     // shift_timestep: read the solution and the state before anything is overwritten
     const int l = S.lanef();
@@ -2972,7 +3002,7 @@ int nmpc_closed_loop_dev(nmpc_handle* h, int32_t B, int32_t K, const double* lbx
                          const double* v_t, const double* w_t, int64_t ld_tk, int64_t ld_tb,
                          const double* p_step, int64_t ld_ps,
                          double* u_hist, double* x_hist, double* f_hist, double* fov_hist,
-                         int32_t* status_hist, int32_t* iters_hist, void* stream) {
+                         int32_t* status_hist, int32_t* iters_hist, const int32_t* order, void* stream) {
   if (!h) return fail(NMPC_E_INVALID, "null handle");
   if (B < 0 || K < 0) return fail(NMPC_E_INVALID, "B < 0 or K < 0");
   if (B == 0 || K == 0) return NMPC_OK;
@@ -2997,6 +3027,7 @@ int nmpc_closed_loop_dev(nmpc_handle* h, int32_t B, int32_t K, const double* lbx
   lp.u_hist = u_hist; lp.x_hist = x_hist; lp.f_hist = f_hist; lp.fov_hist = fov_hist;
   lp.pstep = p_step; lp.ld_ps = ld_ps;
   lp.st_hist = status_hist; lp.it_hist = iters_hist;
+  lp.order = order;
   hipLaunchKernelGGL(h->loop, dim3(B), dim3(WAVE), h->lds_bytes, (hipStream_t)stream,
                      (const Params*)h->dprm, (int)B, io, lp);
   const hipError_t e = hipGetLastError();

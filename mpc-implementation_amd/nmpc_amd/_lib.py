@@ -96,7 +96,7 @@ def lib():
     L.nmpc_read_trace.argtypes = [vp, C.c_int32, dp]
     L.nmpc_shift_dev.argtypes = [vp, C.c_int32, vp, i64, vp, vp, vp, vp, vp]
     L.nmpc_closed_loop_dev.argtypes = ([vp, C.c_int32, C.c_int32] + [vp, i64] * 4 + [vp, i64] + [vp] * 3
-                                       + [i64, i64] + [vp, i64] + [vp] * 7)
+                                       + [i64, i64] + [vp, i64] + [vp] * 8)
     L.nmpc_last_error.argtypes = []
     L.nmpc_last_error.restype = C.c_char_p
     L.nmpc_kernel_info.argtypes = [vp, i32p, i32p]

@@ -224,7 +224,7 @@ class Solver:
                                     C.c_void_p(stream.cuda_stream)))
 
     def closed_loop_device(self, K: int, lbx, ubx, lbg, ubg, p, w, v_t, w_t, hist: dict | None = None,
-                           stream=None, p_step=None):
+                           stream=None, p_step=None, order=None):
         """K closed-loop MPC steps per scenario in one launch (see nmpc_closed_loop_dev).
 
         p (B,np) and w (B,nw) are advanced in place.  Target controls v_t, w_t:
@@ -233,6 +233,8 @@ class Solver:
         u (K,B,6), x (K,B,8), f (K,B), fov (K,B), status/iters (K,B) int32.
         ``p_step`` (K,np), optional: added to p[11:] after each step (moving
         obstacles, targets.obstacle_steps).
+        ``order`` (B,) int32 device tensor, optional: dispatch order, a permutation
+        of range(B) (schedule.longest_first); results do not depend on it.
         """
         import torch
 
@@ -276,6 +278,9 @@ class Solver:
             assert p_step.dtype == torch.float64 and p_step.is_cuda and p_step.is_contiguous()
             assert tuple(p_step.shape) == (K, self.np), (tuple(p_step.shape), (K, self.np))
             ps_ld = self.np
+        if order is not None:
+            assert order.dtype == torch.int32 and order.is_cuda and order.is_contiguous()
+            assert tuple(order.shape) == (B,), tuple(order.shape)
         if stream is None:
             stream = torch.cuda.current_stream()
         _lib.check(L.nmpc_closed_loop_dev(self._h, B, K, *ins, C.c_void_p(p.data_ptr()), self.np,
@@ -284,6 +289,7 @@ class Solver:
                                           C.c_void_p(p_step.data_ptr() if p_step is not None else 0), ps_ld,
                                           op("u"), op("x"),
                                           op("f"), op("fov"), op("status"), op("iters"),
+                                          C.c_void_p(order.data_ptr() if order is not None else 0),
                                           C.c_void_p(stream.cuda_stream)))
 
     def set_trace(self, enable: bool):

@@ -28,3 +28,6 @@ print("ms per chain-iteration if the longest chain bounds the launch:", ms / cha
 print("top chains:", chain[order[:10]].tolist())
 print("scenarios with >=5 max-iter steps:", int(((it >= 100).sum(0) >= 5).sum()))
 print("status counts:", {int(k): int(v) for k, v in zip(*np.unique(st, return_counts=True))})
+out = os.environ.get("CHAIN_OUT")
+if out:
+    np.savez(out, iters=it, status=st, ms=ms)

@@ -1,0 +1,27 @@
+"""Dev tool: cycles per iteration of restoration-heavy solves (the closed-loop
+tail), from the 16 captured restoration cases replicated to B scenarios; needs
+the -DNMPC_STAMPS build (NMPC_LIB=.../libnmpc_amd_stamps.so)."""
+import os, sys, time
+import numpy as np
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "mpc-implementation_amd"))
+from nmpc_amd import nlpsol, make_spec, REFERENCE_OPTS
+B = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
+G = np.load(os.path.join(ROOT, "tests", "golden", "resto_cases.npz"))
+rep = (B + 15) // 16
+W = np.tile(G["w"], (rep, 1))[:B]
+Pm = np.tile(G["p"], (rep, 1))[:B]
+spec = make_spec("race_track_2", N=20, T=0.2)
+lbx, ubx, lbg, ubg = spec.bounds()
+s = nlpsol("solver", "ipopt", spec, REFERENCE_OPTS)
+s.set_trace(True)
+for _ in range(2):
+    t = time.time()
+    s(x0=W.T, lbx=lbx, ubx=ubx, lbg=lbg, ubg=ubg, p=Pm.T)
+    wall = time.time() - t
+tr = s.read_trace(B)
+st = tr[:, s.max_iter:, :].reshape(B, 24)
+it = s.stats()["iter_count"]
+tot = st[:, 15]
+print(f"B={B} wall {wall*1e3:.1f} ms; iters mean {np.mean(it):.1f} max {np.max(it)}; "
+      f"cycles/iter mean {np.mean(tot / it):.3e}; main-phase share {np.mean(st[:, :15].sum(1) / tot):.2f}")

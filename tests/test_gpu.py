@@ -333,6 +333,48 @@ def test_closed_loop_kernel_matches_per_step_launches():
     assert _rel(w2.cpu().numpy(), w1.cpu().numpy()) <= 1e-12
 
 
+def test_closed_loop_dispatch_order_does_not_change_results():
+    """nmpc_closed_loop_dev with a dispatch order (schedule.longest_first of the
+    previous launch's iterations, then a random permutation) gives bitwise the
+    results of index-order dispatch; entries outside [0,B) are skipped."""
+    import torch
+    from nmpc_amd import make_spec
+    from nmpc_amd.schedule import longest_first
+
+    spec = make_spec("race_track_2", N=20, T=0.2)
+    B, K = 80, 3
+    P, bnd, vt, wt = _closed_loop_inputs(spec, B, 1003)
+    f64 = dict(dtype=torch.float64, device="cuda")
+    s = _solver(spec)
+
+    def run(order):
+        p = torch.tensor(P, **f64)
+        w = torch.zeros(B, spec.nw, **f64)
+        hist = {"u": torch.empty(K, B, 6, **f64), "f": torch.empty(K, B, **f64),
+                "status": torch.full((K, B), 99, dtype=torch.int32, device="cuda"),
+                "iters": torch.full((K, B), -1, dtype=torch.int32, device="cuda")}
+        s.closed_loop_device(K, *bnd, p, w, vt, wt, hist, order=order)
+        torch.cuda.synchronize()
+        return {k: v.cpu().numpy() for k, v in hist.items()}, p.cpu().numpy(), w.cpu().numpy()
+
+    ref, p_ref, w_ref = run(None)
+    g = torch.Generator().manual_seed(5)
+    for order in (longest_first(torch.tensor(ref["iters"], device="cuda")),
+                  torch.randperm(B, generator=g).to(torch.int32).cuda()):
+        got, p_got, w_got = run(order)
+        for k in ref:
+            np.testing.assert_array_equal(got[k], ref[k], err_msg=k)
+        np.testing.assert_array_equal(p_got, p_ref)
+        np.testing.assert_array_equal(w_got, w_ref)
+    # out-of-range entries: those workgroups do nothing, the named scenarios still run
+    bad = torch.arange(B, dtype=torch.int32, device="cuda")
+    bad[1] = B + 7
+    bad[2] = -3
+    got, _, _ = run(bad)
+    assert (got["iters"][:, 1] == -1).all() and (got["iters"][:, 2] == -1).all()
+    np.testing.assert_array_equal(got["iters"][:, 3:], ref["iters"][:, 3:])
+
+
 def test_closed_loop_parity_with_oracle_loop():
     """The fused closed loop against the oracle's own solve + shift_timestep loop
     (Python/NMPC_TT.py:348-402 restated) under a target schedule that changes

@@ -165,3 +165,17 @@ def test_dynamic_obstacle_schedule_and_weight_indices():
     assert (s.np, s.w1_pidx, s.w2_pidx) == (13, 11, 12)
     with pytest.raises(ValueError):
         ProblemSpec(N=5, np=13, w1_pidx=3).validate()
+
+
+def test_longest_first_order():
+    """schedule.longest_first: a permutation, largest summed cost first, ties in index order."""
+    import torch
+    from nmpc_amd.schedule import longest_first
+
+    it = torch.tensor([[3, 100, 7, 7, 0], [4, 100, 1, 1, 0]], dtype=torch.int32)
+    o = longest_first(it)
+    assert o.dtype == torch.int32 and o.tolist() == [1, 2, 3, 0, 4]
+    c = torch.tensor([5.0, 9.0, 1.0])
+    assert longest_first(c).tolist() == [1, 0, 2]
+    r = torch.randint(0, 100, (3, 257))
+    assert sorted(longest_first(r).tolist()) == list(range(257))
