@@ -117,6 +117,9 @@ template <int NMAX, int MMAX>
 struct Cap {
   static constexpr int nmax = NMAX, mmax = MMAX;
   static constexpr Lay L = make_layout(NMAX, MMAX);
+  // row passes: trips of 64 rows processed together (their loads batched), <= 5
+  static constexpr int rtrips = (MMAX * (NMAX + 1) + 63) / 64;
+  static constexpr int ru = rtrips < 5 ? rtrips : 5;
 };
 
 // waves per SIMD the kernels are register-budgeted for (256 VGPRs at 2)
@@ -243,11 +246,16 @@ enum Phase { PH_ROLLOUT, PH_EVAL, PH_DERIVS, PH_ADJ, PH_SUMM, PH_RIC, PH_RESOLVE
              PH_RA, PH_RB, PH_RC, PH_RD, PH_RE, PH_SIGX, PH_LSSET, PH_FILT, PH_COUNT };
 #ifdef NMPC_STAMPS
 #define STAMP0() const unsigned long long _ts0 = __builtin_amdgcn_s_memtime()
+#define STAMPV0(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
+#define STAMPV1(v, ph) do { const unsigned long long _tv1 = __builtin_amdgcn_s_memtime(); \
+    if (lanef() == 0) stamps[ph] += (double)(_tv1 - v); } while (0)
 #define STAMP1(ph) do { const unsigned long long _ts1 = __builtin_amdgcn_s_memtime(); \
     if (lanef() == 0) stamps[ph] += (double)(_ts1 - _ts0); } while (0)
 #else
 #define STAMP0() do {} while (0)
 #define STAMP1(ph) do {} while (0)
+#define STAMPV0(v) do {} while (0)
+#define STAMPV1(v, ph) do {} while (0)
 #endif
 
 template <class CAP>
@@ -263,6 +271,24 @@ struct Solver {
   // compiler cannot hoist per-lane address arithmetic of every array out of
   // the main loop (that LICM kept ~200 extra VGPRs live for the whole kernel).
   __device__ __forceinline__ int lanef() const { int x = lane_; asm volatile("" : "+v"(x)); return x; }
+  // Row-parallel pass, latency-batched: rows r = lane + 64 t are visited CAP::ru trips
+  // at a time with a clamped index, f(r, on) with on = (r < ng).  Bodies load every
+  // operand unconditionally and fold masked rows out with selects, so a group of
+  // trips is one basic block whose global loads are all in flight together (a plain
+  // `for (r = lane; r < ng; r += 64)` with loads under `if (hasl(..))` waits on
+  // memory several times per trip).  Per lane the rows are still visited in
+  // increasing order, so reductions are bitwise those of the plain loop.
+  template <class F>
+  __device__ __forceinline__ void rows(F&& f) const {
+    for (int base = 0; base < ng; base += CAP::ru * WAVE) {
+#pragma unroll
+      for (int u = 0; u < CAP::ru; ++u) {
+        const int r = base + u * WAVE + lanef();
+        const bool on = r < ng;
+        f(on ? r : ng - 1, on);
+      }
+    }
+  }
   int N, m, nobs, nw, ng;
   int nb, nuE, nwE;  // box rows per stage; real controls per stage; real decision length
   double T;
@@ -654,55 +680,73 @@ struct Solver {
   __device__ __forceinline__ static int pk8(int i, int j) { return i * (15 - i) / 2 + j; }  // i <= j
   __device__ __forceinline__ void assemble(int mode, double hfac, double gfac, bool dyn) {
     STAMP0();
+    const double kd = P->o.kappa_d;
+    const bool soc = (mode == SUM_SOC || mode == SUM_RESTO_SOC);  // right-hand side only
+    // (a) row-parallel (64 rows per trip instead of m rows per stage lane): each row's
+    //     weight dc^2 A (Q part) and right-hand side dc Bw, into scratch row vectors that
+    //     are dead in every caller at this point (ds2: SOC step, written after the
+    //     solve; dt: trial constraints, rewritten by the next trial)
+    GLB double* Wr = ds2;
+    GLB double* Br = dt;
+    rows([&](int r, bool on) {
+      const double dcr = dc[r];
+      double A, Bw;
+      if (mode == SUM_LS) {
+        A = 1.0;
+        Bw = -(vu[r] - vl[r]);
+      } else if (mode == SUM_LS_RESTO) {
+        // (I + J^T J / 3) w = bx + J^T (bs + bp - bn) / 3 : the restoration NLP's
+        // least-squares multipliers with p, n eliminated
+        A = 1.0 / 3.0;
+        Bw = -((vu[r] - vl[r]) + (rho - zpR[r]) - (rho - znR[r])) / 3.0;
+      } else if (mode == SUM_RESTO || mode == SUM_RESTO_SOC) {
+        double D, rs, Sp, Sn, rp, rn, Dt, Dr;
+        row_resto(r, mode == SUM_RESTO_SOC, D, rs, Sp, Sn, rp, rn, Dt, Dr);
+        A = Dt;
+        Bw = y[r] + Dr;
+      } else {
+        const double sr = s[r], vlr = vl[r], vur = vu[r], yr = y[r];
+        const double rd = (mode == SUM_SOC) ? dms[r] : d[r] - sr;
+        const double lo_ = dl[r], hi_ = du[r];
+        const bool lo = hasl(lo_), hi = hasu(hi_);
+        const double iSl = lo ? rcp(sr - lo_) : 0.0, iSu = hi ? rcp(hi_ - sr) : 0.0;
+        const double D = vlr * iSl + vur * iSu + delta;
+        const double rs = -yr - mu * iSl + mu * iSu +
+                          kd * mu * ((lo && !hi ? 1.0 : 0.0) - (hi && !lo ? 1.0 : 0.0));
+        A = D;
+        Bw = yr + D * rd + rs;
+      }
+      if (on) {
+        if (!soc) Wr[r] = dcr * dcr * A;
+        Br[r] = dcr * Bw;
+      }
+    });
+    sync();
+    // (b) stage-parallel (lane = stage k): fold the stage's rows into Q_k, q_k
     const int k = lanef();
     if (k <= N) {
       const LDS double* xk = X + k * 8;
       double Qxy0 = 0, Qxy1 = 0, Qxy2 = 0, qx = 0, qy = 0;
       double Qb[5] = {0, 0, 0, 0, 0}, qb[5] = {0, 0, 0, 0, 0};
-      const double kd = P->o.kappa_d;
+      const bool curv = !(mode == SUM_LS || mode == SUM_LS_RESTO);  // y-weighted row curvature
       for (int i = 0; i < m; ++i) {
         const int r = k * m + i;
-        double A, Bw, C = 0.0;
-        if (mode == SUM_LS) {
-          A = 1.0;
-          Bw = -(vu[r] - vl[r]);
-        } else if (mode == SUM_LS_RESTO) {
-          // (I + J^T J / 3) w = bx + J^T (bs + bp - bn) / 3 : the restoration NLP's
-          // least-squares multipliers with p, n eliminated
-          A = 1.0 / 3.0;
-          Bw = -((vu[r] - vl[r]) + (rho - zpR[r]) - (rho - znR[r])) / 3.0;
-        } else if (mode == SUM_RESTO || mode == SUM_RESTO_SOC) {
-          double D, rs, Sp, Sn, rp, rn, Dt, Dr;
-          row_resto(r, mode == SUM_RESTO_SOC, D, rs, Sp, Sn, rp, rn, Dt, Dr);
-          A = Dt;
-          Bw = y[r] + Dr;
-          C = y[r] * dc[r];
-        } else {
-          const bool lo = hasl(dl[r]), hi = hasu(du[r]);
-          const double iSl = lo ? rcp(s[r] - dl[r]) : 0.0, iSu = hi ? rcp(du[r] - s[r]) : 0.0;
-          const double D = vl[r] * iSl + vu[r] * iSu + delta;
-          const double rs = -y[r] - mu * iSl + mu * iSu +
-                            kd * mu * ((lo && !hi ? 1.0 : 0.0) - (hi && !lo ? 1.0 : 0.0));
-          const double rd = (mode == SUM_SOC) ? dms[r] : d[r] - s[r];
-          A = D;
-          Bw = y[r] + D * rd + rs;
-          C = y[r] * dc[r];
-        }
+        const double w = soc ? 0.0 : Wr[r], bw = Br[r];
         if (i < nb) {
-          Qb[i] = dc[r] * dc[r] * A;
-          qb[i] = dc[r] * Bw;
+          Qb[i] = w;
+          qb[i] = bw;
         } else {
+          const double C = curv ? y[r] * dc[r] : 0.0;
           const int o = i - nb;
           const double ddx = xk[0] - obx[o], ddy = xk[1] - oby[o];
           const double idd = rsq(ddx * ddx + ddy * ddy);
           const double gx = -(ddx * idd), gy = -(ddy * idd);
           const double id3 = idd * idd * idd;
-          const double w = dc[r] * dc[r] * A;
           Qxy0 += w * gx * gx + C * (-ddy * ddy * id3);
           Qxy1 += w * gx * gy + C * (ddx * ddy * id3);
           Qxy2 += w * gy * gy + C * (-ddx * ddx * id3);
-          qx += dc[r] * Bw * gx;
-          qy += dc[r] * Bw * gy;
+          qx += bw * gx;
+          qy += bw * gy;
         }
       }
       LDS double* qo = qs + k * 10;
@@ -1470,7 +1514,12 @@ __device__ __forceinline__ void resto_phase(const Params* __restrict__ prm, doub
       V[10] = -1e50; V[11] = -1e50;
       V[12] = io.f;            // original (scaled) objective at the restoration iterate
       int rstat = 1;        // 1 running, 0 back to the original problem, else final status
+      auto lanef = [&]() { return S.lanef(); };  // for the STAMP macros
+      (void)lanef;
+      LDS double* stamps = S.stamps;
+      (void)stamps;
       while (true) {
+        STAMP0();
         // ---- progress w.r.t. the original problem (RestoConvergenceCheck)
         if (!firstR) {
           double tho = 0.0;
@@ -1591,7 +1640,9 @@ __device__ __forceinline__ void resto_phase(const Params* __restrict__ prm, doub
           S.mu = V[4];
           S.etaR = o.resto_proximity_weight * sqrt(V[4]);
         }
+        STAMP1(PH_CONV);
         // ---- Newton step of the restoration problem (p, n eliminated per row)
+        { STAMP0();
         for (int i = S.lanef(); i < nw; i += WAVE) {
           const bool hl = S.hasl(S.xl[i]), hu = S.hasu(S.xu[i]);
           const double Sl = hl ? S.U[i] - S.xl[i] : 1.0, Su = hu ? S.xu[i] - S.U[i] : 1.0;
@@ -1601,6 +1652,7 @@ __device__ __forceinline__ void resto_phase(const Params* __restrict__ prm, doub
                     kd * V[4] * ((hl && !hu ? 1.0 : 0.0) - (hu && !hl ? 1.0 : 0.0)));
         }
         sync();
+        STAMP1(PH_SIGX); }
         if (V[9] > 0) V[8] = V[9];
         double dR = 0.0;
         bool fok = false;
@@ -1620,11 +1672,13 @@ __device__ __forceinline__ void resto_phase(const Params* __restrict__ prm, doub
         if (!fok) { rstat = ST_STEP_ERR; break; }
         S.forward(S.dU, S.dX);
         {
+          STAMP0();
           double th, g;
           S.row_step_resto(S.dX, false, S.ds, S.dpR, S.dnR, S.dyR, th, g);
           for (int i = S.lanef(); i < nw; i += WAVE) g += S.ru[i] * S.dU[i];
           V[15] = wsum(th);
           V[16] = wsum(g);
+          STAMP1(PH_ROWSTEP);
         }
         V[17] = S.barrier_obj(0.0, S.U, S.s, nullptr, 0.0) + S.resto_pn_terms(S.U, 0.0, nullptr, nullptr);
         if (V[6] < 0) {
@@ -1657,6 +1711,7 @@ __device__ __forceinline__ void resto_phase(const Params* __restrict__ prm, doub
           if (V[15] <= V[7]) amin = fmin(amin, o.delta * pow(V[15], o.s_theta) / pow(-V[16], o.s_phi));
         }
         amin *= o.alpha_min_frac;
+        STAMPV0(_tls);
         V[18] = S.frac_to_bound_resto(V[5], S.dU, S.ds, S.dpR, S.dnR);
         double a = V[18];
         V[19] = 0.0; V[20] = 0.0; V[21] = 0.0;
@@ -1697,9 +1752,11 @@ __device__ __forceinline__ void resto_phase(const Params* __restrict__ prm, doub
           a *= o.alpha_red_factor;
           ++nsteps;
         }
+        STAMPV1(_tls, PH_INIT);
         if (acc == 0) { rstat = ST_RESTO_FAIL; break; }  // no restoration inside the restoration phase
         // filter augmentation (F-type + Armijo steps do not augment)
         {
+          STAMP0();
           const GLB double* dUa = (acc == 2) ? S.dU2 : S.dU;
           const GLB double* dsa = (acc == 2) ? S.ds2 : S.ds;
           const GLB double* dpa = (acc == 2) ? S.dp2R : S.dpR;
@@ -1748,6 +1805,7 @@ __device__ __forceinline__ void resto_phase(const Params* __restrict__ prm, doub
           }
           sync();
           V[12] = V[20];
+          STAMP1(PH_ACCEPT);
           S.derivs(S.X, S.U);
           ++it;
           if (trace && S.lanef() == 0) {
@@ -2079,25 +2137,29 @@ __device__ __forceinline__ int solve_one(Solver<CAP>& S, const Params* __restric
       if (S.hasu(S.xu[i])) cmp = fmax(cmp, fabs((S.xu[i] - S.U[i]) * S.zu[i]));
       sumz += fabs(S.zl[i]) + fabs(S.zu[i]);
     }
-    for (int r = S.lanef(); r < ng; r += WAVE) {
-      const double g = -S.y[r] - S.vl[r] + S.vu[r];
-      dinf = fmax(dinf, fabs(g));
+    S.rows([&](int r, bool on) {
+      const double yr = S.y[r], vlr = S.vl[r], vur = S.vu[r], dr = S.d[r], sr = S.s[r], dcr = S.dc[r];
+      const double lo = S.dl[r], hi = S.du[r];
+      const bool hl = on && S.hasl(lo), hu = on && S.hasu(hi);
+      const double g = -yr - vlr + vur;
+      if (on) dinf = fmax(dinf, fabs(g));
       double cv = 0.0;
-      if (S.hasl(S.dl[r])) {
-        cv = fmax(cv, S.dl[r] - S.d[r]);
-        cmp = fmax(cmp, fabs((S.s[r] - S.dl[r]) * S.vl[r]));
+      if (hl) cv = fmax(cv, lo - dr);
+      const double cl = fabs((sr - lo) * vlr);
+      if (hl) cmp = fmax(cmp, cl);
+      if (hu) cv = fmax(cv, dr - hi);
+      const double cu = fabs((hi - sr) * vur);
+      if (hu) cmp = fmax(cmp, cu);
+      const double ucv = cv / dcr;
+      if (on) {
+        cviol = fmax(cviol, cv);
+        ucviol = fmax(ucviol, ucv);
+        pinf = fmax(pinf, fabs(dr - sr));
+        sumy += fabs(yr);
+        sumv += fabs(vlr) + fabs(vur);
+        if (!isfinite(dr) || !isfinite(g)) bad = true;
       }
-      if (S.hasu(S.du[r])) {
-        cv = fmax(cv, S.d[r] - S.du[r]);
-        cmp = fmax(cmp, fabs((S.du[r] - S.s[r]) * S.vu[r]));
-      }
-      cviol = fmax(cviol, cv);
-      ucviol = fmax(ucviol, cv / S.dc[r]);
-      pinf = fmax(pinf, fabs(S.d[r] - S.s[r]));
-      sumy += fabs(S.y[r]);
-      sumv += fabs(S.vl[r]) + fabs(S.vu[r]);
-      if (!isfinite(S.d[r]) || !isfinite(g)) bad = true;
-    }
+    });
     dinf = wmax(dinf); cviol = wmax(cviol); ucviol = wmax(ucviol); cmp = wmax(cmp);
     pinf = wmax(pinf);
     sumy = wsum(sumy); sumz = wsum(sumz); sumv = wsum(sumv);

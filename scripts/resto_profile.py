@@ -25,3 +25,11 @@ it = s.stats()["iter_count"]
 tot = st[:, 15]
 print(f"B={B} wall {wall*1e3:.1f} ms; iters mean {np.mean(it):.1f} max {np.max(it)}; "
       f"cycles/iter mean {np.mean(tot / it):.3e}; main-phase share {np.mean(st[:, :15].sum(1) / tot):.2f}")
+PH = ["rollout", "eval", "derivs", "adjoint", "summaries", "riccati", "resolve", "forward", "row_step",
+      "barrier", "ftb", "dual_ftb", "conv+mu", "accept", "init/resto-ls", "TOTAL", "ric.1", "#factor", "#soc",
+      "ric.2", "ric.3", "sigx", "ls_setup", "filter"]
+mi = np.mean(it)
+for i, n in enumerate(PH):
+    if i in (15, 17, 18):
+        continue
+    print(f"  {n:14s} per-iter {st[:, i].mean() / mi:10.1f}  {100 * st[:, i].mean() / tot.mean():6.2f}%")
