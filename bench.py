@@ -37,6 +37,11 @@ HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md chip table
 KFLOP_PER_STAGE_ITER = 7.5   # ~6.2k Riccati + ~1k assembly per stage-iteration
 
 
+# BASELINE.json "metric" (the headline number is quoted on its config 3: 4096
+# scenarios per GPU, N=20, 10 obstacles)
+METRIC = "MPC steps/sec (batched scenarios), N=20 9-state UAV, 1/2/4/8 MI355X"
+
+
 def survey_bytes_per_step(spec, ibar):
     """SURVEY.md 8(d) streamed-KKT byte model (fp64)."""
     nx, nu, m, N = 8, 6, spec.m, spec.N
@@ -287,12 +292,15 @@ def main():
                     "per_step": "warm-started closed-loop MPC steps, one launch per step",
                     "cold": "cold-start (u=0) solves, one launch per step"}[args.mode]
         res = {
-            "metric": "MPC steps/sec (batched scenarios), N=20 UAV+gimbal, 10 obstacles",
+            "metric": METRIC,
             "value": value, "unit": "MPC steps/s", "n_gpus": world, "steps": K,
             "warmup": W, "ms_per_step": ms_per_step, "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
-            "config": {"workload": f"config {args.config}: batch={B}/GPU, N={spec.N}, {spec.n_obs} static "
-                                   f"obstacles (Race Track 2.py), T={spec.T}, reference IPOPT opts, {mode_txt}",
+            "config": {"workload": f"config {args.config}: batch={B}/GPU, "
+                                   f"{'no-gimbal 5-state' if spec.model == 'uav5' else '8-state UAV+gimbal'}, "
+                                   f"N={spec.N}, {spec.n_obs} static obstacles"
+                                   f"{' (Race Track 2.py layout)' if spec.n_obs else ''}, T={spec.T}, "
+                                   f"reference IPOPT opts, {mode_txt}",
                        "global_batch": B * world, "seq_len": spec.N, "parallelism": f"dp{world}"},
             "roofline": {"bound": "hbm", "achieved": achieved_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved_gbs / HBM_PEAK_GBS, "traffic": traffic,

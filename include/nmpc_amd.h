@@ -63,7 +63,7 @@ enum {
   NMPC_MODEL_UAV5 = 1   /* no gimbal: 5 states / 3 controls, distance cost, rows [z, theta] (+ obstacles),
                            MATLAB/Dynamic Obstacles/NMPC_TT.m:26-35,102-111,129-134; w = vec(U) with U
                            3 x N, p = [x0(5); xs(3); ...], X_out 5 x (N+1); w2 is ignored.
-                           Per-step entry points only (nmpc_shift_dev / nmpc_closed_loop_dev reject it) */
+                           All entry points, including nmpc_shift_dev / nmpc_closed_loop_dev */
 };
 
 /* IPOPT options honoured by the solver (names and meaning as IPOPT's;
@@ -161,7 +161,8 @@ int nmpc_read_trace(nmpc_handle* h, int32_t B, double* host_out);
  * warm start u <- [u(:,2:N), u(:,N)], target xs <- xs + T [v cos, v sin, w].
  * p (np x B, ld_p) is updated in place (x0 = p[0:8], xs = p[8:11]); w_out
  * (nw x B) receives the shifted warm start; v_t, w_t (length B) are the target
- * speeds (Python/NMPC_TT.py:25). */
+ * speeds (Python/NMPC_TT.py:25).  No-gimbal model: x0 = p[0:5], xs = p[5:8],
+ * 3 controls per stage (MATLAB/Dynamic Obstacles/shift1.m). */
 int nmpc_shift_dev(nmpc_handle* h, int32_t B, double* p, int64_t ld_p,
                    const double* u_sol, double* w_out,
                    const double* v_t, const double* w_t, void* stream);
@@ -183,6 +184,10 @@ int nmpc_shift_dev(nmpc_handle* h, int32_t B, double* p, int64_t ld_p,
  * DEVICE pointers, enqueued on `stream`.
  *   p   : np x B (ld_p >= np), in/out (advanced K steps)
  *   w   : nw x B (ld nw), in: first warm start; out: the last step's shifted solution
+ *   No-gimbal model: the same loop on [x0(5); xs(3)] and 3 controls per stage
+ *   (MATLAB/Dynamic Obstacles/NMPC_TT.m:150-183, shift1.m); histories keep the
+ *   widths below with absent gimbal entries 0, and the FOV centre of a camera
+ *   without gimbal angles is the UAV's ground position (x, y).
  *   u_hist K x B x 6, x_hist K x B x 8, f_hist / fov_hist / status_hist /
  *   iters_hist K x B; each nullable.  Bounds as in nmpc_solve_batch_dev.
  *   order: nullable, B int32 (device): a permutation of 0..B-1 giving the order in

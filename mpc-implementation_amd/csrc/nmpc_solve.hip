@@ -2635,7 +2635,8 @@ __global__ __launch_bounds__(WAVE, NMPC_WAVES_PER_EU) void nmpc_closed_loop_kern
   // of slots (an out-of-range entry is skipped, never dereferenced)
   const int b = lp.order ? lp.order[blockIdx.x] : (int)blockIdx.x;
   if (b < 0 || b >= B) return;
-  const int nw = prm->nw;
+  // caller layout (external): w = nwE = nuE*N decisions, p = [x0(nxE); xs(3); ...]
+  const int nw = prm->nwE, nu = prm->nuE, nx = prm->nxE;
   const double T = prm->T;
   double* wb = lp.w + (long long)b * nw;
   double* pb = lp.p + (long long)b * lp.ld_p;
@@ -2669,34 +2670,37 @@ __global__ __launch_bounds__(WAVE, NMPC_WAVES_PER_EU) void nmpc_closed_loop_kern
 #pragma unroll
     for (int j = 0; j < WR; ++j) {
       const int i = l + j * WAVE;
-      wn[j] = i < nw ? wb[i + 6 < nw ? i + 6 : i] : 0.0;
+      wn[j] = i < nw ? wb[i + nu < nw ? i + nu : i] : 0.0;
     }
-    const int npar = prm->np;
+    const int npar = prm->npE;
     double pv = l < npar ? pb[l] : 0.0;
-    const double u0 = l < 6 ? wb[l] : 0.0;
-    if (lp.x_hist && l < 8) lp.x_hist[(kb + b) * 8 + l] = pv;
+    const double u0 = l < nu ? wb[l] : 0.0;
+    // histories keep the gimbal model's widths (8 states, 6 controls); an absent
+    // state / control of the no-gimbal model is recorded as 0
+    if (lp.x_hist && l < 8) lp.x_hist[(kb + b) * 8 + l] = l < nx ? pv : 0.0;
     if (lp.u_hist && l < 6) lp.u_hist[(kb + b) * 6 + l] = u0;
-    const double th = readlane_d(pv, 3), ps = readlane_d(pv, 4), xs2 = readlane_d(pv, 10);
+    const double th = readlane_d(pv, 3), ps = readlane_d(pv, 4), xs2 = readlane_d(pv, nx + 2);
     const double v = readlane_d(u0, 0);
-    // x0 <- x0 + T f(x0, u0): [v c(psi) c(th), v s(psi) c(th), v s(th), u1..u5]
-    const double ush = __shfl(u0, l >= 3 && l < 8 ? l - 2 : 0, WAVE);
+    // x0 <- x0 + T f(x0, u0): [v c(psi) c(th), v s(psi) c(th), v s(th), u1..u(nx-3)]
+    const double ush = __shfl(u0, l >= 3 && l < nx ? l - 2 : 0, WAVE);
     double fx = 0.0;
     if (l == 0) fx = v * cos(ps) * cos(th);
     else if (l == 1) fx = v * sin(ps) * cos(th);
     else if (l == 2) fx = v * sin(th);
-    else if (l < 8) fx = ush;
-    else if (l == 8) fx = lp.vt[k * lp.ld_tk + b * lp.ld_tb] * cos(xs2);
-    else if (l == 9) fx = lp.vt[k * lp.ld_tk + b * lp.ld_tb] * sin(xs2);
-    else if (l == 10) fx = lp.wt[k * lp.ld_tk + b * lp.ld_tb];
+    else if (l < nx) fx = ush;
+    else if (l == nx) fx = lp.vt[k * lp.ld_tk + b * lp.ld_tb] * cos(xs2);
+    else if (l == nx + 1) fx = lp.vt[k * lp.ld_tk + b * lp.ld_tb] * sin(xs2);
+    else if (l == nx + 2) fx = lp.wt[k * lp.ld_tk + b * lp.ld_tb];
     sync();
     const double pnew = pv + T * fx;
-    if (l < 11) pb[l] = pnew;
+    if (l < nx + 3) pb[l] = pnew;
     else if (l < npar && lp.pstep) pb[l] = pv + lp.pstep[k * lp.ld_ps + l];  // moving obstacles etc.
     if (lp.fov_hist) {
-      // FOV centre of the new state vs the target before its step
+      // FOV centre of the new state vs the target before its step; without a gimbal
+      // (x5 = x6 = 0) it is the UAV's ground position (x, y)
       const double x1 = readlane_d(pnew, 0), y1 = readlane_d(pnew, 1), z1 = readlane_d(pnew, 2);
-      const double g5 = readlane_d(pnew, 5), g6 = readlane_d(pnew, 6);
-      const double xt = readlane_d(pv, 8), yt = readlane_d(pv, 9);
+      const double g5 = nx > 5 ? readlane_d(pnew, 5) : 0.0, g6 = nx > 5 ? readlane_d(pnew, 6) : 0.0;
+      const double xt = readlane_d(pv, nx), yt = readlane_d(pv, nx + 1);
       const double hv = prm->hv, hh = prm->hh;
       const double ap = (z1 * tan(g6 + hv) - z1 * tan(g6 - hv)) / 2;
       const double bp = (z1 * tan(g5 + hh) - z1 * tan(g5 - hh)) / 2;
@@ -2713,27 +2717,28 @@ __global__ __launch_bounds__(WAVE, NMPC_WAVES_PER_EU) void nmpc_closed_loop_kern
 }
 
 // closed-loop shift kernel (Python/NMPC_TT.py:13-30): one thread per scenario
-__global__ void nmpc_shift_kernel(int B, int N, int np, double T, double* p, long long ld_p,
+// nx / nu: the model's (external) state / control counts, 8 / 6 with gimbal,
+// 5 / 3 without (MATLAB/Dynamic Obstacles/shift1.m: the same step on [x0(5); xs(3)])
+__global__ void nmpc_shift_kernel(int B, int N, int nx, int nu, double T, double* p, long long ld_p,
                                   const double* u, double* w_out, const double* vt, const double* wt) {
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= B) return;
   double* pb = p + (long long)b * ld_p;
-  const double* ub = u + (long long)b * 6 * N;
+  const double* ub = u + (long long)b * nu * N;
   const double th = pb[3], ps = pb[4], v = ub[0];
   const double f0 = v * cos(ps) * cos(th), f1 = v * sin(ps) * cos(th), f2 = v * sin(th);
   pb[0] = pb[0] + T * f0; pb[1] = pb[1] + T * f1; pb[2] = pb[2] + T * f2;
-  for (int c = 0; c < 5; ++c) pb[3 + c] = pb[3 + c] + T * ub[1 + c];
-  double* wb = w_out + (long long)b * 6 * N;
+  for (int c = 3; c < nx; ++c) pb[c] = pb[c] + T * ub[c - 2];
+  double* wb = w_out + (long long)b * nu * N;
   for (int k = 0; k < N; ++k) {
     const int src = (k + 1 < N) ? k + 1 : N - 1;
-    for (int c = 0; c < 6; ++c) wb[k * 6 + c] = ub[src * 6 + c];
+    for (int c = 0; c < nu; ++c) wb[k * nu + c] = ub[src * nu + c];
   }
-  const double xs2 = pb[10];
+  const double xs2 = pb[nx + 2];
   const double vv = vt[b], ww = wt[b];
-  pb[8] = pb[8] + T * (vv * cos(xs2));
-  pb[9] = pb[9] + T * (vv * sin(xs2));
-  pb[10] = pb[10] + T * ww;
-  (void)np;
+  pb[nx] = pb[nx] + T * (vv * cos(xs2));
+  pb[nx + 1] = pb[nx + 1] + T * (vv * sin(xs2));
+  pb[nx + 2] = pb[nx + 2] + T * ww;
 }
 
 // ------------------------------------------------------------------ host side
@@ -3048,11 +3053,10 @@ int nmpc_shift_dev(nmpc_handle* h, int32_t B, double* p, int64_t ld_p, const dou
   if (!h) return fail(NMPC_E_INVALID, "null handle");
   if (B <= 0) return B == 0 ? NMPC_OK : fail(NMPC_E_INVALID, "B < 0");
   if (!p || !u_sol || !w_out || !v_t || !w_t) return fail(NMPC_E_INVALID, "null pointer");
-  if (h->hp.model != NMPC_MODEL_UAV8G) return fail(NMPC_E_INVALID, "shift: gimbal model only");
-  if (ld_p < h->hp.np) return fail(NMPC_E_INVALID, "ld_p < np");
+  if (ld_p < h->hp.npE) return fail(NMPC_E_INVALID, "ld_p < np");
   const int thr = 256;
   hipLaunchKernelGGL(nmpc_shift_kernel, dim3((B + thr - 1) / thr), dim3(thr), 0, (hipStream_t)stream, (int)B,
-                     h->hp.N, h->hp.np, h->hp.T, p, (long long)ld_p, u_sol, w_out, v_t, w_t);
+                     h->hp.N, h->hp.nxE, h->hp.nuE, h->hp.T, p, (long long)ld_p, u_sol, w_out, v_t, w_t);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return fail(NMPC_E_HIP, std::string("shift launch: ") + hipGetErrorString(e));
   return NMPC_OK;
@@ -3073,9 +3077,8 @@ int nmpc_closed_loop_dev(nmpc_handle* h, int32_t B, int32_t K, const double* lbx
   if (ld_tk < 0 || ld_tb < 0) return fail(NMPC_E_INVALID, "negative target-schedule stride");
   if (p_step && ld_ps < 0) return fail(NMPC_E_INVALID, "negative p_step stride");
   const Params& P = h->hp;
-  if (P.model != NMPC_MODEL_UAV8G) return fail(NMPC_E_INVALID, "closed loop: gimbal model only");
   if ((ld_lbx != 0 && ld_lbx < P.nw) || (ld_ubx != 0 && ld_ubx < P.nw) || (ld_lbg != 0 && ld_lbg < P.ng) ||
-      (ld_ubg != 0 && ld_ubg < P.ng) || ld_p < P.np)
+      (ld_ubg != 0 && ld_ubg < P.ng) || ld_p < P.npE)
     return fail(NMPC_E_INVALID, "leading dimension smaller than the vector length");
   if ((long long)B * K > (1LL << 40)) return fail(NMPC_E_INVALID, "B*K too large");
   IO io;

@@ -553,14 +553,73 @@ def test_no_gimbal_model_parity(layout, N, seed):
             assert abs(sol["f"][0, b] - r["f"]) <= TOL * (1 + abs(r["f"]))
 
 
-def test_no_gimbal_model_entry_points():
-    from nmpc_amd import make_spec, _lib
+def test_no_gimbal_shift_matches_oracle():
+    """nmpc_shift_dev on the no-gimbal model: MATLAB/Dynamic Obstacles/shift1.m
+    (x0 <- x0 + T f5(x0, u0), u shifted by one stage of 3 controls, target
+    unicycle step with con_t = [15; 0.12]) against the oracle's shift_timestep."""
     import torch
+    from nmpc_amd import make_spec, draw_scenarios
 
     spec = make_spec(None, N=10, T=0.2, model="uav5")
-    s = _solver(spec)
+    prob = orc.make_problem(None, N=10, T=0.2, model="uav5")
+    B = 5
+    rng = np.random.default_rng(3)
+    P = draw_scenarios(spec, B, seed=11)
+    lbx, ubx, _, _ = spec.bounds()
+    U = lbx + (ubx - lbx) * rng.random((B, spec.nw))
     f64 = dict(dtype=torch.float64, device="cuda")
-    B = 2
-    with pytest.raises(_lib.NmpcError):
-        s.shift_device(torch.zeros(B, spec.np, **f64), torch.zeros(B, spec.nw, **f64),
-                       torch.zeros(B, spec.nw, **f64), torch.zeros(B, **f64), torch.zeros(B, **f64))
+    p, u = torch.tensor(P, **f64), torch.tensor(U, **f64)
+    w = torch.zeros(B, spec.nw, **f64)
+    s = _solver(spec)
+    s.shift_device(p, u, w, torch.full((B,), 15.0, **f64), torch.full((B,), 0.12, **f64))
+    torch.cuda.synchronize()
+    for b in range(B):
+        x1, u1, xs1 = orc.shift_timestep(prob, P[b, :5], U[b].reshape(10, 3).T, P[b, 5:8], con_t=(15.0, 0.12))
+        assert _rel(p[b, :5].cpu().numpy(), x1) <= 1e-14
+        assert _rel(p[b, 5:8].cpu().numpy(), xs1) <= 1e-14
+        np.testing.assert_array_equal(w[b].cpu().numpy(), u1.T.ravel())
+
+
+def test_no_gimbal_closed_loop_matches_oracle_loop():
+    """The fused closed loop on the no-gimbal model (MATLAB/Dynamic Obstacles/NMPC_TT.m
+    main loop :150-183 with shift1.m) against the oracle's solve + shift loop on the
+    true 3N-variable problem: statuses, applied controls, states and the FOV-centre
+    error, which without gimbal angles is the UAV-target ground distance."""
+    import torch
+    from nmpc_amd import make_spec
+
+    N, B, K = 10, 3, 3
+    spec = make_spec(None, N=N, T=0.2, model="uav5")
+    P, bnd, _, _ = _closed_loop_inputs(spec, B, 1001)
+    f64 = dict(dtype=torch.float64, device="cuda")
+    vt, wt = torch.full((B,), 15.0, **f64), torch.full((B,), 0.12, **f64)
+    s = _solver(spec)
+    p = torch.tensor(P, **f64)
+    w = torch.zeros(B, spec.nw, **f64)
+    hist = {"u": torch.empty(K, B, 6, **f64), "x": torch.empty(K, B, 8, **f64),
+            "fov": torch.empty(K, B, **f64), "status": torch.empty(K, B, dtype=torch.int32, device="cuda")}
+    s.closed_loop_device(K, *bnd, p, w, vt, wt, hist)
+    torch.cuda.synchronize()
+    prob = orc.make_problem(None, N=N, T=0.2, model="uav5")
+    ref = orc.IpoptDense(prob, orc.REFERENCE_OPTS)
+    lbx, ubx, lbg, ubg = spec.bounds()
+    H = {k: v.cpu().numpy() for k, v in hist.items()}
+    checked = 0
+    for b in range(B):
+        x0, xs, u0 = P[b, :5].copy(), P[b, 5:8].copy(), np.zeros(spec.nw)
+        for k in range(K):
+            np.testing.assert_allclose(H["x"][k, b, :5], x0, rtol=1e-9, atol=1e-9)
+            assert (H["x"][k, b, 5:] == 0).all() and (H["u"][k, b, 3:] == 0).all()
+            r = ref.solve(u0, lbx, ubx, lbg, ubg, np.concatenate([x0, xs]))
+            assert int(H["status"][k, b]) == r["status"], (b, k)
+            if r["status"] != 0:
+                break
+            assert _rel(H["u"][k, b, :3], r["x"][:3]) <= TOL
+            x1, u1, xs1 = orc.shift_timestep(prob, x0, r["x"].reshape(N, 3).T, xs, con_t=(15.0, 0.12))
+            d = np.hypot(x1[0] - xs[0], x1[1] - xs[1])
+            assert abs(H["fov"][k, b] - d) <= 1e-6 * (1 + d), (b, k, H["fov"][k, b], d)
+            x0, u0, xs = x1, u1.T.ravel(), xs1
+            checked += 1
+    assert checked >= B
+
+
