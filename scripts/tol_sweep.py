@@ -1,0 +1,91 @@
+"""Tolerance sweep (SURVEY f2 "tol sweep"; BASELINE config 5 names fp32-vs-fp64):
+throughput and accuracy of the fp64 solver at IPOPT tol / acceptable_tol in
+{1e-8 (the reference's), 1e-6, 1e-4}, on config 3 (N=20, 10 obstacles) and
+config 5 (N=50, dynamic obstacles, moving per the MATLAB schedule).
+
+Per (config, tol):
+  * cold solve of step 0 (same inputs for every tol): launch time, mean
+    iterations, status histogram, and the deviation of the applied control u0
+    and of the objective from the tol=1e-8 solution (scenarios where both
+    report Solve_Succeeded);
+  * fused closed loop of K steps: MPC steps/s (longest-first dispatch from a
+    one-step warm-up).
+Writes one JSON object per line to stdout.
+usage: python scripts/tol_sweep.py [B3] [B5] [K]"""
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "mpc-implementation_amd"))
+from nmpc_amd import nlpsol, config_spec, draw_scenarios, REFERENCE_OPTS  # noqa: E402
+from nmpc_amd.schedule import longest_first  # noqa: E402
+from nmpc_amd.targets import obstacle_steps  # noqa: E402
+
+B3 = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
+B5 = int(sys.argv[2]) if len(sys.argv) > 2 else 8192
+K = int(sys.argv[3]) if len(sys.argv) > 3 else 10
+f64 = dict(dtype=torch.float64, device="cuda")
+i32 = dict(dtype=torch.int32, device="cuda")
+
+
+def opts(tol):
+    o = {"ipopt": dict(REFERENCE_OPTS["ipopt"]), "print_time": 0}
+    o["ipopt"]["tol"] = tol
+    o["ipopt"]["acceptable_tol"] = max(tol, REFERENCE_OPTS["ipopt"]["acceptable_tol"])
+    return o
+
+
+def timed(fn):
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    e0.record()
+    fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1)
+
+
+for cfg, B in ((3, B3), (5, B5)):
+    spec = config_spec(cfg)
+    P = torch.tensor(draw_scenarios(spec, B, seed=1000 + cfg), **f64)
+    bnd = [torch.tensor(v, **f64) for v in spec.bounds()]
+    vt, wt = torch.full((B,), 12.0, **f64), torch.full((B,), 0.01, **f64)
+    pstep = torch.tensor(obstacle_steps(0, K + 1, spec.np), **f64) if cfg == 5 else None
+    ref = None
+    for tol in (1e-8, 1e-6, 1e-4):
+        s = nlpsol("solver", "ipopt", spec, opts(tol))
+        out = {"x": torch.empty(B, spec.nw, **f64), "f": torch.empty(B, **f64),
+               "status": torch.empty(B, **i32), "iters": torch.empty(B, **i32)}
+        w0 = torch.zeros(B, spec.nw, **f64)
+        s.solve_device(w0, *bnd, P, out)  # warm-up (code objects, workspace)
+        ms = timed(lambda: s.solve_device(w0, *bnd, P, out))
+        x, f = out["x"].cpu().numpy(), out["f"].cpu().numpy()
+        st, it = out["status"].cpu().numpy(), out["iters"].cpu().numpy()
+        rec = {"config": cfg, "batch": B, "N": spec.N, "tol": tol, "dtype": "f64",
+               "cold_solve_ms": ms, "cold_mean_iters": float(it.mean()),
+               "cold_status": {int(k): int(v) for k, v in zip(*np.unique(st, return_counts=True))}}
+        if ref is None:
+            ref = (x, f, st)
+        else:
+            ok = (st == 0) & (ref[2] == 0)
+            du = np.abs(x[ok, :6] - ref[0][ok, :6]) / (1.0 + np.abs(ref[0][ok, :6]))
+            df = np.abs(f[ok] - ref[1][ok]) / (1.0 + np.abs(ref[1][ok]))
+            rec.update({"u0_rel_dev_max": float(du.max()), "u0_rel_dev_p99": float(np.percentile(du.max(1), 99)),
+                        "f_rel_dev_max": float(df.max()), "compared": int(ok.sum())})
+        # fused closed loop: 1 warm-up step (its iterations order the dispatch), then K timed
+        p, w = P.clone(), torch.zeros(B, spec.nw, **f64)
+        h1 = {"iters": torch.empty(1, B, **i32)}
+        s.closed_loop_device(1, *bnd, p, w, vt, wt, h1, p_step=None if pstep is None else pstep[:1].contiguous())
+        order = longest_first(h1["iters"])
+        hk = {"iters": torch.empty(K, B, **i32), "status": torch.empty(K, B, **i32)}
+        pk = None if pstep is None else pstep[1:].contiguous()
+        s.closed_loop_device(K, *bnd, p.clone(), w.clone(), vt, wt, hk, p_step=pk, order=order)
+        ms_cl = timed(lambda: s.closed_loop_device(K, *bnd, p, w, vt, wt, hk, p_step=pk, order=order))
+        rec.update({"closed_loop_steps": K, "closed_loop_ms": ms_cl,
+                    "closed_loop_mpc_steps_per_s": B * K / (ms_cl / 1e3),
+                    "closed_loop_mean_iters": float(hk["iters"].double().mean().item())})
+        print(json.dumps(rec), flush=True)
