@@ -119,7 +119,7 @@ struct Cap {
   static constexpr Lay L = make_layout(NMAX, MMAX);
   // row passes: trips of 64 rows processed together (their loads batched), <= 5
   static constexpr int rtrips = (MMAX * (NMAX + 1) + 63) / 64;
-  static constexpr int ru = rtrips < 5 ? rtrips : 5;
+  static constexpr int ru = rtrips < 2 ? rtrips : 2;
 };
 
 // waves per SIMD the kernels are register-budgeted for (256 VGPRs at 2)
@@ -796,13 +796,14 @@ struct Solver {
   }
 
   // ----------------------------------------- Riccati factorisation + solve
-  // Backward sweep over stages, lanef() (i,j) owning entry (i,j) of the 8x8
-  // cost-to-go matrix, three LDS exchanges per stage:
+  // Backward sweep over stages, lane (i,j) owning entry (i,j) of the 8x8
+  // cost-to-go matrix, two LDS exchanges per stage:
   //   (1) A^T P A (register), S~ = S + B^T P A and R~ = R + B^T P B (21 lanes)
   //       straight from P (A = I + E, B = [b0 | T e_3..7]);
-  //   (2) every lanef(): Cholesky of R~ (inertia: all pivots > 0); lanes 0..7:
-  //       column j of K = -R~^{-1} S~, lanef() 8: k = -R~^{-1} r~ (two triangular solves);
-  //   (3) P_k = Q_k + A^T P A + S~^T K ; p_k = q_k + A^T p + K^T r~.
+  //   (2) every lane: Cholesky R~ = L L^T (inertia: all pivots > 0) and Y = L^-1 S~
+  //       for its columns i, j: P_k = Q_k + A^T P A - Y_i^T Y_j (= ... + S~^T K);
+  //       lanes 0..7: column j of K = -L^-T Y_j, p_k = q_k + A^T p + K^T r~;
+  //       lane 8: k = -R~^{-1} r~.
   // Stores K_k, k_k and R~_k (for the gradient-only re-solve).
   __device__ __forceinline__ bool riccati(const GLB double* Rd, const GLB double* rv) {
 #ifdef NMPC_STAMPS
@@ -814,16 +815,18 @@ struct Solver {
     return r;
   }
   __device__ __forceinline__ bool riccati_(const GLB double* Rd, const GLB double* rv) {
-    const int i = lanef() >> 3, j = lanef() & 7;
+    // one opaque lane index for the whole sweep (every lanef() call is a fresh register copy)
+    const int ln = lanef();
+    const int i = ln >> 3, j = ln & 7;
     const int ij = (i <= j) ? pk8(i, j) : pk8(j, i);
     LDS double* Pc = Pa;
     LDS double* Pn = Pb;
     LDS double* pc = pva;
     LDS double* pn = pvb;
-    Pc[lanef()] = Qs[N * 36 + ij];
-    if (lanef() < 8) pc[lanef()] = qs[N * 10 + lanef()];
+    Pc[ln] = Qs[N * 36 + ij];
+    if (ln < 8) pc[ln] = qs[N * 10 + ln];
     // lanes 48..63 -> R~ entries t = 0..15, lanes 0..4 -> t = 16..20 (packed lower)
-    const int tR = lanef() >= 48 ? lanef() - 48 : (lanef() < 5 ? 16 + lanef() : -1);
+    const int tR = ln >= 48 ? ln - 48 : (ln < 5 ? 16 + ln : -1);
     int rR = 0;
     while (tR >= 0 && (rR + 1) * (rR + 2) / 2 <= tR) ++rR;
     const int cR = tR >= 0 ? tR - rR * (rR + 1) / 2 : 0;
@@ -832,10 +835,14 @@ struct Solver {
     // the recursion: fetch stage k-1's while stage k is formed, so the sweep never
     // waits on a global load.  Lanes 0..5 hold r_k (broadcast by readlane).
     const bool diagR = tR >= 0 && rR == cR;
-    const int lr = lanef() < 6 ? lanef() : 5;
+    const int lr = ln < 6 ? ln : 5;
     double qvn = Qs[(N - 1) * 36 + ij];
     double rdn = (diagR && Rd) ? Rd[(N - 1) * 6 + rR] : 1.0;
     double rvn = rv[(N - 1) * 6 + lr];
+    // P_k is symmetric: lane (i,j) with i <= j forms entry (i,j) and stores it to both
+    // halves; lane 8 = (1,0) is then free to carry r~ through the triangular solves
+    const bool upper = i <= j;
+    const int ji = j * 8 + i;
     sync();
     bool ok = true;
     for (int k = N - 1; k >= 0; --k) {
@@ -858,7 +865,7 @@ struct Solver {
       { STAMP0();
         const double P00 = Pc[0], P01 = Pc[1], P02 = Pc[2], P11 = Pc[9], P12 = Pc[10], P22 = Pc[18];
         const double P0j = Pc[j], P1j = Pc[8 + j], P2j = Pc[16 + j];
-        const double Pi0 = Pc[i * 8], Pi1 = Pc[i * 8 + 1], Pi2 = Pc[i * 8 + 2], Pij = Pc[lanef()];
+        const double Pi0 = Pc[i * 8], Pi1 = Pc[i * 8 + 1], Pi2 = Pc[i * 8 + 2], Pij = Pc[ln];
         const double PA0j = P0j + ((P00 * aj0 + P01 * aj1) + P02 * aj2);
         const double PA1j = P1j + ((P01 * aj0 + P11 * aj1) + P12 * aj2);
         const double PA2j = P2j + ((P02 * aj0 + P12 * aj1) + P22 * aj2);
@@ -868,7 +875,7 @@ struct Solver {
         const double PArj = Prj + ((Pr0 * aj0 + Pr1 * aj1) + Pr2 * aj2);
         double stv = (i == 0) ? ((b00 * PA0j + b10 * PA1j) + b20 * PA2j) : T * PArj;
         stv += (i == 0 && j == 3) ? qs[k * 10 + 8] : ((i == 0 && j == 4) ? qs[k * 10 + 9] : 0.0);
-        if (lanef() < 48) St[lanef()] = stv;
+        if (ln < 48) St[ln] = stv;
         if (tR >= 0) {
           double v;
           if (rR == 0) {  // b0^T P[0:3,0:3] b0
@@ -913,51 +920,54 @@ struct Solver {
         rt[0] = readlane_d(rvk, 0) + ((b00 * pc[0] + b10 * pc[1]) + b20 * pc[2]);
 #pragma unroll
         for (int r = 1; r < 6; ++r) rt[r] = readlane_d(rvk, r) + T * pc[2 + r];
-        if (lanef() < 9) {
-          // column lanef() of K = -R~^{-1} S~ (lane 8: k = -R~^{-1} r~) by two
-          // triangular solves with the Cholesky factor
-          double v[6];
+        double ya[6], yb[6];
 #pragma unroll
-          for (int r = 0; r < 6; ++r) {
-            double a = (lanef() < 8) ? St[r * 8 + lanef()] : rt[r];
+        for (int r = 0; r < 6; ++r) {
+          double a = St[r * 8 + i];
+          double bb = (ln == 8) ? rt[r] : St[r * 8 + j];
 #pragma unroll
-            for (int t = 0; t < r; ++t) a -= Lm[r * (r + 1) / 2 + t] * v[t];
-            v[r] = a * idg[r];
+          for (int t = 0; t < r; ++t) {
+            a -= Lm[r * (r + 1) / 2 + t] * ya[t];
+            bb -= Lm[r * (r + 1) / 2 + t] * yb[t];
           }
+          ya[r] = a * idg[r];
+          yb[r] = bb * idg[r];
+        }
+        if (upper) {
+          double sy = 0.0;
+#pragma unroll
+          for (int r = 0; r < 6; ++r) sy += ya[r] * yb[r];
+          const double pv = (qv + APA) - sy;
+          Pn[ln] = pv;
+          Pn[ji] = pv;
+        }
+        if (ln < 9) {
 #pragma unroll
           for (int r = 5; r >= 0; --r) {
-            double a = v[r];
+            double a = yb[r];
 #pragma unroll
-            for (int t = r + 1; t < 6; ++t) a -= Lm[t * (t + 1) / 2 + r] * v[t];
-            v[r] = a * idg[r];
+            for (int t = r + 1; t < 6; ++t) a -= Lm[t * (t + 1) / 2 + r] * yb[t];
+            yb[r] = a * idg[r];
           }
+          if (ln < 8) {
 #pragma unroll
-          for (int r = 0; r < 6; ++r) {
-            if (lanef() < 8) { Kc[r * 8 + lanef()] = -v[r]; K[k * 48 + r * 8 + lanef()] = -v[r]; }
-            else kf[k * 6 + r] = -v[r];
+            for (int r = 0; r < 6; ++r) K[k * 48 + r * 8 + ln] = -yb[r];
+            double atp = pc[ln];
+            if (ln == 3) atp = atp + ((E03 * pc[0] + E13 * pc[1]) + E23 * pc[2]);
+            else if (ln == 4) atp = atp + (E04 * pc[0] + E14 * pc[1]);
+            double kr = 0.0;
+#pragma unroll
+            for (int r = 0; r < 6; ++r) kr += (-yb[r]) * rt[r];
+            pn[ln] = (qs[k * 10 + ln] + atp) + kr;
+          } else {
+#pragma unroll
+            for (int r = 0; r < 6; ++r) kf[k * 6 + r] = -yb[r];
           }
         }
         sync();
         STAMP1(PH_RD); }
-      ok = !wany(!ok);  // every lanef() computed the same pivots; make it explicit
+      ok = !wany(!ok);  // every lane computed the same pivots; make it explicit
       if (!ok) break;
-      // ---- (3)
-      { STAMP0();
-        double sk = 0.0;
-#pragma unroll
-        for (int r = 0; r < 6; ++r) sk += St[r * 8 + i] * Kc[r * 8 + j];
-        Pn[lanef()] = (qv + APA) + sk;
-        if (lanef() < 8) {
-          double atp = pc[lanef()];
-          if (lanef() == 3) atp = atp + ((E03 * pc[0] + E13 * pc[1]) + E23 * pc[2]);
-          else if (lanef() == 4) atp = atp + (E04 * pc[0] + E14 * pc[1]);
-          double kr = 0.0;
-#pragma unroll
-          for (int r = 0; r < 6; ++r) kr += Kc[r * 8 + lanef()] * rt[r];
-          pn[lanef()] = (qs[k * 10 + lanef()] + atp) + kr;
-        }
-        sync();
-        STAMP1(PH_RE); }
       LDS double* t1 = Pc; Pc = Pn; Pn = t1;
       LDS double* t2 = pc; pc = pn; pn = t2;
     }
@@ -1040,30 +1050,34 @@ struct Solver {
   // carries dx redundantly.  Lane 0 stores dX.
   __device__ __forceinline__ void forward(GLB double* dUo, LDS double* dXo) {
     STAMP0();
+    const int ln = lanef();
     double dx[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) dx[i] = 0.0;
-    if (lanef() < 8) dXo[lanef()] = 0.0;
-    const int r = lanef() < 6 ? lanef() : 5;
+    if (ln < 8) dXo[ln] = 0.0;
+    const int r = ln < 6 ? ln : 5;
     // K_k rows come from global memory and do not depend on dx: fetch stage k+1's
     // row while stage k is being formed
     double Kn[8];
 #pragma unroll
     for (int c = 0; c < 8; ++c) Kn[c] = K[r * 8 + c];
+    double kn = kf[r];
     for (int k = 0; k < N; ++k) {
       double Kr[8];
 #pragma unroll
       for (int c = 0; c < 8; ++c) Kr[c] = Kn[c];
+      const double kk = kn;
       if (k + 1 < N) {
 #pragma unroll
         for (int c = 0; c < 8; ++c) Kn[c] = K[(k + 1) * 48 + r * 8 + c];
+        kn = kf[(k + 1) * 6 + r];
       }
       double E03, E04, E13, E14, E23, b00, b10, b20;
       stage_AB(k, E03, E04, E13, E14, E23, b00, b10, b20);
-      double a = kf[k * 6 + r];
+      double a = kk;
 #pragma unroll
       for (int c = 0; c < 8; ++c) a += Kr[c] * dx[c];
-      if (lanef() < 6) dUo[k * 6 + lanef()] = a;
+      if (ln < 6) dUo[k * 6 + ln] = a;
       double du_[6];
 #pragma unroll
       for (int q = 0; q < 6; ++q) du_[q] = readlane_d(a, q);
@@ -1073,7 +1087,7 @@ struct Solver {
       xn[2] = dx[2] + E23 * dx[3] + b20 * du_[0];
 #pragma unroll
       for (int c = 0; c < 5; ++c) xn[3 + c] = dx[3 + c] + T * du_[1 + c];
-      if (lanef() == 0) {
+      if (ln == 0) {
 #pragma unroll
         for (int c = 0; c < 8; ++c) dXo[(k + 1) * 8 + c] = xn[c];
       }
@@ -1114,30 +1128,31 @@ struct Solver {
     STAMP0();
     const double kd = P->o.kappa_d;
     th = 0.0; g = 0.0; msv = 0.0;
-    for (int r = lanef(); r < ng; r += WAVE) {
+    rows([&](int r, bool on) {
       const int k = r / m, i = r - k * m;
+      const double dcr = dc[r], sr = s[r], dr = d[r], lo = dl[r], hi = du[r];
       const LDS double* xk = X + k * 8;
       const LDS double* dxk = dXs + k * 8;
       double jd;
       if (i < nb) {
-        jd = dc[r] * dxk[boxidx(i)];
+        jd = dcr * dxk[boxidx(i)];
       } else {
         const int o = i - nb;
         const double ddx = xk[0] - obx[o], ddy = xk[1] - oby[o];
         const double idd = rsq(ddx * ddx + ddy * ddy);
-        jd = dc[r] * ((-(ddx * idd)) * dxk[0] + (-(ddy * idd)) * dxk[1]);
+        jd = dcr * ((-(ddx * idd)) * dxk[0] + (-(ddy * idd)) * dxk[1]);
       }
-      const double sr = s[r], dr = d[r];
       const double dsr = jd + (dr - sr);
-      ds[r] = dsr;
-      th += fabs(dr - sr);
-      const double lo = dl[r], hi = du[r];
+      if (on) ds[r] = dsr;
       const bool hl = hasl(lo), hu = hasu(hi);
       const double gs = -(hl ? mu_ / (sr - lo) : 0.0) + (hu ? mu_ / (hi - sr) : 0.0) +
                         kd * mu_ * ((hl && !hu ? 1.0 : 0.0) - (hu && !hl ? 1.0 : 0.0));
-      g += gs * dsr;
-      msv = fmax(msv, fabs(dsr / (1.0 + fabs(sr))));
-    }
+      if (on) {
+        th += fabs(dr - sr);
+        g += gs * dsr;
+        msv = fmax(msv, fabs(dsr / (1.0 + fabs(sr))));
+      }
+    });
     STAMP1(PH_ROWSTEP);
     sync();
   }
@@ -1272,11 +1287,12 @@ struct Solver {
       if (hasl(xl[i]) && dx < 0) a = fmin(a, (-tau_ * (U[i] - xl[i])) / dx);
       if (hasu(xu[i]) && -dx < 0) a = fmin(a, (-tau_ * (xu[i] - U[i])) / (-dx));
     }
-    for (int r = lanef(); r < ng; r += WAVE) {
-      const double dd = dss[r];
-      if (hasl(dl[r]) && dd < 0) a = fmin(a, (-tau_ * (s[r] - dl[r])) / dd);
-      if (hasu(du[r]) && -dd < 0) a = fmin(a, (-tau_ * (du[r] - s[r])) / (-dd));
-    }
+    rows([&](int r, bool on) {
+      const double dd = dss[r], sr = s[r], lo = dl[r], hi = du[r];
+      const double al = (-tau_ * (sr - lo)) / dd, au = (-tau_ * (hi - sr)) / (-dd);
+      if (on && hasl(lo) && dd < 0) a = fmin(a, al);
+      if (on && hasu(hi) && -dd < 0) a = fmin(a, au);
+    });
     a = wmin(a);
     STAMP1(PH_FTB);
     return a;
@@ -1302,12 +1318,16 @@ struct Solver {
       if (hasl(xl[i]) && a1 < 0) a = fmin(a, (-tau_ * zl[i]) / a1);
       if (hasu(xu[i]) && a2 < 0) a = fmin(a, (-tau_ * zu[i]) / a2);
     }
-    for (int r = lanef(); r < ng; r += WAVE) {
-      double a1, a2;
-      dv_s(r, dss[r], a1, a2);
-      if (hasl(dl[r]) && a1 < 0) a = fmin(a, (-tau_ * vl[r]) / a1);
-      if (hasu(du[r]) && a2 < 0) a = fmin(a, (-tau_ * vu[r]) / a2);
-    }
+    rows([&](int r, bool on) {
+      const double sr = s[r], lo = dl[r], hi = du[r], vlr = vl[r], vur = vu[r], dsv = dss[r];
+      const bool hl = hasl(lo), hu = hasu(hi);
+      double a1 = 0.0, a2 = 0.0;  // dv_s with the loads hoisted
+      if (hl) { const double iS = rcp(sr - lo); a1 = mu * iS - vlr - vlr * iS * dsv; }
+      if (hu) { const double iS = rcp(hi - sr); a2 = mu * iS - vur + vur * iS * dsv; }
+      const double b1 = (-tau_ * vlr) / a1, b2 = (-tau_ * vur) / a2;
+      if (on && hl && a1 < 0) a = fmin(a, b1);
+      if (on && hu && a2 < 0) a = fmin(a, b2);
+    });
     a = wmin(a);
     STAMP1(PH_DFTB);
     return a;
@@ -1329,10 +1349,12 @@ struct Solver {
       if (hasl(xl[i])) c = fmax(c, fabs((U[i] - xl[i]) * zl[i] - mu_));
       if (hasu(xu[i])) c = fmax(c, fabs((xu[i] - U[i]) * zu[i] - mu_));
     }
-    for (int r = lanef(); r < ng; r += WAVE) {
-      if (hasl(dl[r])) c = fmax(c, fabs((s[r] - dl[r]) * vl[r] - mu_));
-      if (hasu(du[r])) c = fmax(c, fabs((du[r] - s[r]) * vu[r] - mu_));
-    }
+    rows([&](int r, bool on) {
+      const double sr = s[r], lo = dl[r], hi = du[r], vlr = vl[r], vur = vu[r];
+      const double cl = fabs((sr - lo) * vlr - mu_), cu = fabs((hi - sr) * vur - mu_);
+      if (on && hasl(lo)) c = fmax(c, cl);
+      if (on && hasu(hi)) c = fmax(c, cu);
+    });
     return wmax(c);
   }
 
@@ -2500,22 +2522,31 @@ __device__ __forceinline__ int solve_one(Solver<CAP>& S, const Params* __restric
         else nzu = 0.0;
         S.zl[i] = nzl; S.zu[i] = nzu;
       }
-      for (int r = S.lanef(); r < ng; r += WAVE) {
-        double D, rs, dvl, dvu;
-        S.row_rs(r, D, rs);
-        S.dv_s(r, dsa[r], dvl, dvu);
-        const double dyv = D * dsa[r] + rs;
-        const double sn = S.s[r] + ap * dsa[r];
-        double nvl = S.vl[r] + ad * dvl, nvu = S.vu[r] + ad * dvu;
-        if (S.hasl(S.dl[r])) { const double Sn = sn - S.dl[r]; nvl = fmax(fmin(nvl, ks * mu / Sn), mu / (ks * Sn)); }
+      const double kdm = o.kappa_d * S.mu, dlt = S.delta;
+      S.rows([&](int r, bool on) {
+        const double sr = S.s[r], yr = S.y[r], vlr = S.vl[r], vur = S.vu[r], dsr = dsa[r], dtr = S.dt[r];
+        const double lo = S.dl[r], hi = S.du[r];
+        const bool hl = S.hasl(lo), hu = S.hasu(hi);
+        // row_rs and dv_s (same arithmetic), loads hoisted
+        const double iSl = hl ? rcp(sr - lo) : 0.0, iSu = hu ? rcp(hi - sr) : 0.0;
+        const double D = vlr * iSl + vur * iSu + dlt;
+        const double rs = -yr - S.mu * iSl + S.mu * iSu + kdm * ((hl && !hu ? 1.0 : 0.0) - (hu && !hl ? 1.0 : 0.0));
+        const double dvl = hl ? S.mu * iSl - vlr - vlr * iSl * dsr : 0.0;
+        const double dvu = hu ? S.mu * iSu - vur + vur * iSu * dsr : 0.0;
+        const double dyv = D * dsr + rs;
+        const double sn = sr + ap * dsr;
+        double nvl = vlr + ad * dvl, nvu = vur + ad * dvu;
+        if (hl) { const double Sn = sn - lo; nvl = fmax(fmin(nvl, ks * mu / Sn), mu / (ks * Sn)); }
         else nvl = 0.0;
-        if (S.hasu(S.du[r])) { const double Sn = S.du[r] - sn; nvu = fmax(fmin(nvu, ks * mu / Sn), mu / (ks * Sn)); }
+        if (hu) { const double Sn = hi - sn; nvu = fmax(fmin(nvu, ks * mu / Sn), mu / (ks * Sn)); }
         else nvu = 0.0;
-        S.y[r] = S.y[r] + ap * dyv;
-        S.vl[r] = nvl; S.vu[r] = nvu;
-        S.s[r] = sn;
-        S.d[r] = S.dt[r];
-      }
+        if (on) {
+          S.y[r] = yr + ap * dyv;
+          S.vl[r] = nvl; S.vu[r] = nvu;
+          S.s[r] = sn;
+          S.d[r] = dtr;
+        }
+      });
       for (int i = S.lanef(); i < nw; i += WAVE) S.U[i] = S.Ut[i];
       if (S.lanef() <= N) {
 #pragma unroll
