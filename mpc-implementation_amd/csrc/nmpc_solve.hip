@@ -2295,6 +2295,7 @@ __device__ __forceinline__ int solve_one(Solver<CAP>& S, const Params* __restric
       tiny_msv = wmax(msv);
       STAMP1(PH_LSSET);
     }
+    STAMPV0(_tls);  // whole line search incl. nested phases (diagnostic slot of the old Riccati step 3)
     const double phi_ref = S.barrier_obj(f, S.U, S.s, nullptr, 0.0);
     if (MV[0] < 0) {
       MV[0] = o.theta_max_fact * fmax(1.0, theta_ref);
@@ -2502,6 +2503,7 @@ __device__ __forceinline__ int solve_one(Solver<CAP>& S, const Params* __restric
       break;  // to the restoration phase below the iteration loop
     }
 
+    STAMPV1(_tls, PH_RE);
     // ===== accept the trial point (IpoptAlgorithm::AcceptTrialPoint)
     {
       STAMP0();

@@ -6,7 +6,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "mpc-implementation_amd"))
 from nmpc_amd import nlpsol, config_spec, draw_scenarios, REFERENCE_OPTS
 PH = ["rollout", "eval", "derivs", "adjoint", "summaries", "riccati", "resolve", "forward", "row_step",
-      "barrier", "ftb", "dual_ftb", "conv+mu", "accept", "init", "TOTAL", "ric.1", "#factor", "#soc", "ric.2", "ric.3", "sigx", "ls_setup", "filter"]
+      "barrier", "ftb", "dual_ftb", "conv+mu", "accept", "init", "TOTAL", "ric.1", "#factor", "#soc", "ric.2", "ls-total", "sigx", "ls_setup", "filter"]
 cfg = int(sys.argv[1]) if len(sys.argv) > 1 else 3
 B = int(sys.argv[2]) if len(sys.argv) > 2 else 4096
 spec = config_spec(cfg)
