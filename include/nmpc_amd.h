@@ -205,6 +205,15 @@ int nmpc_closed_loop_dev(nmpc_handle* h, int32_t B, int32_t K,
                          double* u_hist, double* x_hist, double* f_hist, double* fov_hist,
                          int32_t* status_hist, int32_t* iters_hist, const int32_t* order, void* stream);
 
+/* Scheduling of the last nmpc_closed_loop_dev launch (diagnostics; synchronises the
+ * device when sched_err is requested).  policy: 0 = one workgroup per scenario running
+ * its K steps back to back (B <= resident waves, or NMPC_CLOSED_LOOP=static);
+ * 1 = step queues: persistent waves claim (scenario, step) pairs whose previous step is
+ * done, lowest step first, each scenario pinned to one XCD.  resident: waves the
+ * closed-loop kernel keeps resident (occupancy x CUs; 0 before the first launch).
+ * sched_err: 1 if a wave gave up waiting for a published step (not expected). */
+int nmpc_closed_loop_info(nmpc_handle* h, int32_t* policy, int32_t* resident, int32_t* sched_err);
+
 const char* nmpc_last_error(void);
 
 /* Launch geometry / workspace of the last solve, for measurement. */

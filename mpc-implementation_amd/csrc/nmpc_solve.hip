@@ -2564,9 +2564,6 @@ __device__ __forceinline__ int solve_one(Solver<CAP>& S, const Params* __restric
       }
     }
     ++it;
-#ifdef NMPC_PRIO
-    if (it == NMPC_PRIO) __builtin_amdgcn_s_setprio(3);
-#endif
     if (trace && S.lanef() == 0) {
       double th = 0.0;
       for (int r = 0; r < ng; ++r) th += fabs(S.d[r] - S.s[r]);
@@ -2659,94 +2656,234 @@ struct Loop {
   const int* order;                  // dispatch order: workgroup g runs scenario order[g] (nullable)
 };
 
+// One closed-loop step k of scenario b (Python/NMPC_TT.py:348-402 main loop body):
+// solve with the warm start w and p, record (x0, u0, f, status, iters), then
+// shift_timestep (:13-30).  Everything it reads comes from global memory, so any
+// wavefront can run any (scenario, step) once step k-1 of that scenario is done.
 template <class CAP>
-__global__ __launch_bounds__(WAVE, NMPC_WAVES_PER_EU) void nmpc_closed_loop_kernel(const Params* __restrict__ prm, int B, IO io,
-                                                                    Loop lp) {
-  extern __shared__ __attribute__((aligned(16))) double smem[];
-  // longest-expected-first dispatch: workgroups start roughly in blockIdx order, so a
-  // caller-supplied permutation puts the longest closed-loop chains on the first wave
-  // of slots (an out-of-range entry is skipped, never dereferenced)
-  const int b = lp.order ? lp.order[blockIdx.x] : (int)blockIdx.x;
-  if (b < 0 || b >= B) return;
+__device__ __forceinline__ void cl_step(const Params* __restrict__ prm, int B, const IO& io, const Loop& lp,
+                                        const int b, const int k, double* smem) {
   // caller layout (external): w = nwE = nuE*N decisions, p = [x0(nxE); xs(3); ...]
   const int nw = prm->nwE, nu = prm->nuE, nx = prm->nxE;
   const double T = prm->T;
   double* wb = lp.w + (long long)b * nw;
   double* pb = lp.p + (long long)b * lp.ld_p;
   constexpr int WR = (6 * CAP::nmax + WAVE - 1) / WAVE;
-  int cum_it = 0;
-  (void)cum_it;
-  for (int k = 0; k < lp.K; ++k) {
-    // a fresh solver per step: no member is live across steps (a solver kept
-    // outside the loop costs ~40 VGPRs of spills)
-    Solver<CAP> S;
-    S.bind(prm, smem, io.ws, threadIdx.x, b);
-    IO ik = io;
-    ik.x0 = lp.w; ik.ld_x0 = nw; ik.x_out = lp.w;
-    ik.p = lp.p; ik.ld_p = lp.ld_p;
-    const long long kb = (long long)k * B;
-    ik.f_out = lp.f_hist ? lp.f_hist + kb : nullptr;
-    ik.status = lp.st_hist ? lp.st_hist + kb : nullptr;
-    ik.iters = lp.it_hist ? lp.it_hist + kb : nullptr;
-    const int its = solve_one<CAP>(S, prm, ik, b);
-#ifdef NMPC_PRIO
-    cum_it += its;
-    if (cum_it > 30 * (k + 1)) __builtin_amdgcn_s_setprio(2);
-    else __builtin_amdgcn_s_setprio(0);
-#else
-    (void)its;
-#endif
-    sync();
-    // shift_timestep: read the solution and the state before anything is overwritten
-    const int l = S.lanef();
-    double wn[WR];
+  // a fresh solver per step: no member is live across steps (a solver kept
+  // outside the loop costs ~40 VGPRs of spills)
+  Solver<CAP> S;
+  S.bind(prm, smem, io.ws, threadIdx.x, b);
+  IO ik = io;
+  ik.x0 = lp.w; ik.ld_x0 = nw; ik.x_out = lp.w;
+  ik.p = lp.p; ik.ld_p = lp.ld_p;
+  const long long kb = (long long)k * B;
+  ik.f_out = lp.f_hist ? lp.f_hist + kb : nullptr;
+  ik.status = lp.st_hist ? lp.st_hist + kb : nullptr;
+  ik.iters = lp.it_hist ? lp.it_hist + kb : nullptr;
+  solve_one<CAP>(S, prm, ik, b);
+  sync();
+  // shift_timestep: read the solution and the state before anything is overwritten
+  const int l = S.lanef();
+  double wn[WR];
 #pragma unroll
-    for (int j = 0; j < WR; ++j) {
-      const int i = l + j * WAVE;
-      wn[j] = i < nw ? wb[i + nu < nw ? i + nu : i] : 0.0;
-    }
-    const int npar = prm->npE;
-    double pv = l < npar ? pb[l] : 0.0;
-    const double u0 = l < nu ? wb[l] : 0.0;
-    // histories keep the gimbal model's widths (8 states, 6 controls); an absent
-    // state / control of the no-gimbal model is recorded as 0
-    if (lp.x_hist && l < 8) lp.x_hist[(kb + b) * 8 + l] = l < nx ? pv : 0.0;
-    if (lp.u_hist && l < 6) lp.u_hist[(kb + b) * 6 + l] = u0;
-    const double th = readlane_d(pv, 3), ps = readlane_d(pv, 4), xs2 = readlane_d(pv, nx + 2);
-    const double v = readlane_d(u0, 0);
-    // x0 <- x0 + T f(x0, u0): [v c(psi) c(th), v s(psi) c(th), v s(th), u1..u(nx-3)]
-    const double ush = __shfl(u0, l >= 3 && l < nx ? l - 2 : 0, WAVE);
-    double fx = 0.0;
-    if (l == 0) fx = v * cos(ps) * cos(th);
-    else if (l == 1) fx = v * sin(ps) * cos(th);
-    else if (l == 2) fx = v * sin(th);
-    else if (l < nx) fx = ush;
-    else if (l == nx) fx = lp.vt[k * lp.ld_tk + b * lp.ld_tb] * cos(xs2);
-    else if (l == nx + 1) fx = lp.vt[k * lp.ld_tk + b * lp.ld_tb] * sin(xs2);
-    else if (l == nx + 2) fx = lp.wt[k * lp.ld_tk + b * lp.ld_tb];
-    sync();
-    const double pnew = pv + T * fx;
-    if (l < nx + 3) pb[l] = pnew;
-    else if (l < npar && lp.pstep) pb[l] = pv + lp.pstep[k * lp.ld_ps + l];  // moving obstacles etc.
-    if (lp.fov_hist) {
-      // FOV centre of the new state vs the target before its step; without a gimbal
-      // (x5 = x6 = 0) it is the UAV's ground position (x, y)
-      const double x1 = readlane_d(pnew, 0), y1 = readlane_d(pnew, 1), z1 = readlane_d(pnew, 2);
-      const double g5 = nx > 5 ? readlane_d(pnew, 5) : 0.0, g6 = nx > 5 ? readlane_d(pnew, 6) : 0.0;
-      const double xt = readlane_d(pv, nx), yt = readlane_d(pv, nx + 1);
-      const double hv = prm->hv, hh = prm->hh;
-      const double ap = (z1 * tan(g6 + hv) - z1 * tan(g6 - hv)) / 2;
-      const double bp = (z1 * tan(g5 + hh) - z1 * tan(g5 - hh)) / 2;
-      const double xe = x1 + ap + z1 * tan(g6 - hv), ye = y1 + bp + z1 * tan(g5 - hh);
-      if (l == 0) lp.fov_hist[kb + b] = sqrt((xe - xt) * (xe - xt) + (ye - yt) * (ye - yt));
-    }
-#pragma unroll
-    for (int j = 0; j < WR; ++j) {
-      const int i = l + j * WAVE;
-      if (i < nw) wb[i] = wn[j];
-    }
-    sync();
+  for (int j = 0; j < WR; ++j) {
+    const int i = l + j * WAVE;
+    wn[j] = i < nw ? wb[i + nu < nw ? i + nu : i] : 0.0;
   }
+  const int npar = prm->npE;
+  double pv = l < npar ? pb[l] : 0.0;
+  const double u0 = l < nu ? wb[l] : 0.0;
+  // histories keep the gimbal model's widths (8 states, 6 controls); an absent
+  // state / control of the no-gimbal model is recorded as 0
+  if (lp.x_hist && l < 8) lp.x_hist[(kb + b) * 8 + l] = l < nx ? pv : 0.0;
+  if (lp.u_hist && l < 6) lp.u_hist[(kb + b) * 6 + l] = u0;
+  const double th = readlane_d(pv, 3), ps = readlane_d(pv, 4), xs2 = readlane_d(pv, nx + 2);
+  const double v = readlane_d(u0, 0);
+  // x0 <- x0 + T f(x0, u0): [v c(psi) c(th), v s(psi) c(th), v s(th), u1..u(nx-3)]
+  const double ush = __shfl(u0, l >= 3 && l < nx ? l - 2 : 0, WAVE);
+  double fx = 0.0;
+  if (l == 0) fx = v * cos(ps) * cos(th);
+  else if (l == 1) fx = v * sin(ps) * cos(th);
+  else if (l == 2) fx = v * sin(th);
+  else if (l < nx) fx = ush;
+  else if (l == nx) fx = lp.vt[k * lp.ld_tk + b * lp.ld_tb] * cos(xs2);
+  else if (l == nx + 1) fx = lp.vt[k * lp.ld_tk + b * lp.ld_tb] * sin(xs2);
+  else if (l == nx + 2) fx = lp.wt[k * lp.ld_tk + b * lp.ld_tb];
+  sync();
+  const double pnew = pv + T * fx;
+  if (l < nx + 3) pb[l] = pnew;
+  else if (l < npar && lp.pstep) pb[l] = pv + lp.pstep[k * lp.ld_ps + l];  // moving obstacles etc.
+  if (lp.fov_hist) {
+    // FOV centre of the new state vs the target before its step; without a gimbal
+    // (x5 = x6 = 0) it is the UAV's ground position (x, y)
+    const double x1 = readlane_d(pnew, 0), y1 = readlane_d(pnew, 1), z1 = readlane_d(pnew, 2);
+    const double g5 = nx > 5 ? readlane_d(pnew, 5) : 0.0, g6 = nx > 5 ? readlane_d(pnew, 6) : 0.0;
+    const double xt = readlane_d(pv, nx), yt = readlane_d(pv, nx + 1);
+    const double hv = prm->hv, hh = prm->hh;
+    const double ap = (z1 * tan(g6 + hv) - z1 * tan(g6 - hv)) / 2;
+    const double bp = (z1 * tan(g5 + hh) - z1 * tan(g5 - hh)) / 2;
+    const double xe = x1 + ap + z1 * tan(g6 - hv), ye = y1 + bp + z1 * tan(g5 - hh);
+    if (l == 0) lp.fov_hist[kb + b] = sqrt((xe - xt) * (xe - xt) + (ye - yt) * (ye - yt));
+  }
+#pragma unroll
+  for (int j = 0; j < WR; ++j) {
+    const int i = l + j * WAVE;
+    if (i < nw) wb[i] = wn[j];
+  }
+  sync();
+}
+
+// K-step closed loop, one workgroup per scenario running its K steps back to back.
+template <class CAP>
+__global__ __launch_bounds__(WAVE, NMPC_WAVES_PER_EU) void nmpc_closed_loop_kernel(const Params* __restrict__ prm, int B, IO io,
+                                                                    Loop lp) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  // workgroups start roughly in blockIdx order, so a caller-supplied permutation sets
+  // the order in which scenarios begin (an out-of-range entry is skipped)
+  const int b = lp.order ? lp.order[blockIdx.x] : (int)blockIdx.x;
+  if (b < 0 || b >= B) return;
+  for (int k = 0; k < lp.K; ++k) cl_step<CAP>(prm, B, io, lp, b, k, smem);
+}
+
+// ---- step-queue scheduler for the K-step closed loop (persistent waves)
+// A launch is bounded by its longest scenario chain (K steps of up to max_iter
+// iterations each).  With more scenarios than resident waves, a long chain that only
+// starts after the first wave of slots has drained finishes last, and which chains
+// will be long is hard to predict.  Here every resident wave repeatedly claims the next
+// (scenario, step) whose previous step is done, lowest step index first: a scenario
+// that has fallen behind (a long chain) is served as soon as its previous step ends,
+// so the launch approaches its longest chain without knowing it in advance.
+//  * Queue (x, j) receives each scenario of XCD set x exactly once, when its step j-1
+//    is done; queue (x, 0) is the dispatch order.  Scenarios are pinned to an XCD
+//    (set x = dispatch position mod NXCD) and served only by waves running on that XCD
+//    (hardware register XCC_ID): the per-XCD L2s are not coherent with each other, so
+//    a scenario's state (p, w, histories) is only ever handed between waves sharing
+//    an L2, through agent-scope release / acquire fences.
+//  * Claims and publishes are agent-scope atomics by lane 0.
+//  * Exit: a wave leaves once every queue of its set is fully claimed.  A claimed slot
+//    always has a running writer, so waiting on it is short; a wave that waits longer
+//    than kSchedWaitTicks anyway sets err and leaves instead of spinning forever.
+constexpr int NXCD = 8;  // MI355X: 8 XCDs
+struct SchedQ {
+  int* head;  // NXCD x K: claimed count of queue (x, j)
+  int* tail;  // NXCD x K: published count
+  int* resv;  // NXCD x K: reserved count
+  int* ring;  // NXCD x K x BX scenario ids (-1 = not yet written)
+  int* err;   // 1: a wave gave up waiting
+  int BX;     // ring capacity per queue = ceil(B / NXCD)
+};
+constexpr unsigned long long kSchedWaitTicks = 6000000000ull;  // s_memrealtime (100 MHz): 60 s
+
+// polling loads: relaxed (no L1 invalidation per poll); the claim is followed by one
+// acquire fence.  A scenario never leaves its XCD, so its state only has to reach the
+// XCD's L2: the writer waits for its stores (vmcnt(0), L1 is write-through) before
+// publishing, the reader invalidates its L1 after claiming.  No L2 write-back
+// (an agent-scope release fence flushes the whole L2: measured 20x slower).
+__device__ __forceinline__ int ld_acq(int* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void stores_done() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+__device__ __forceinline__ int xcc_id() {
+  unsigned x;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(x));
+  return (int)(x % NXCD);
+}
+
+template <class CAP>
+__global__ __launch_bounds__(WAVE, NMPC_WAVES_PER_EU) void nmpc_closed_loop_sched_kernel(const Params* __restrict__ prm, int B,
+                                                                          IO io, Loop lp, SchedQ q) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  const int K = lp.K;
+  const int x = xcc_id();
+  const int nset = (B - x + NXCD - 1) / NXCD;  // scenarios in this XCD's set
+  int* head = q.head + x * K;
+  int* tail = q.tail + x * K;
+  int* resv = q.resv + x * K;
+  int* ring = q.ring + (long long)x * K * q.BX;
+  int jmin = 0;
+  for (;;) {
+    int cb = -1, ck = -1;
+    if (threadIdx.x == 0) {
+      const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+      for (;;) {
+        bool all_claimed = true, gave_up = false;
+        for (int j = jmin; j < K; ++j) {
+          const int h = ld_acq(head + j);
+          if (h >= nset) {
+            if (j == jmin) ++jmin;
+            continue;
+          }
+          all_claimed = false;
+          if (h >= ld_acq(tail + j)) continue;  // nothing published in this queue yet
+          int e = h;
+          if (!__hip_atomic_compare_exchange_strong(head + j, &e, h + 1, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                    __HIP_MEMORY_SCOPE_AGENT)) {
+            --j;  // lost the race for this queue: look at it again
+            continue;
+          }
+          // published count > h: slot h's writer has reserved it and stores it next
+          int v = ld_acq(ring + (long long)j * q.BX + h);
+          while (v < 0 && __builtin_amdgcn_s_memrealtime() - t0 < kSchedWaitTicks) {
+            __builtin_amdgcn_s_sleep(2);
+            v = ld_acq(ring + (long long)j * q.BX + h);
+          }
+          if (v < 0) gave_up = true;
+          else { cb = v; ck = j; }
+          break;
+        }
+        if (ck >= 0 || all_claimed) break;
+        if (gave_up || __builtin_amdgcn_s_memrealtime() - t0 > kSchedWaitTicks) {
+          __hip_atomic_store(q.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(127);
+      }
+    }
+    cb = __builtin_amdgcn_readfirstlane(cb);
+    ck = __builtin_amdgcn_readfirstlane(ck);
+    if (ck < 0) break;
+    if (cb >= 0 && cb < B) {  // an out-of-range dispatch entry is claimed and skipped
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // the previous step's p, w (L1 invalidated)
+      cl_step<CAP>(prm, B, io, lp, cb, ck, smem);
+      stores_done();  // this step's p, w, histories are in the XCD's L2
+    }
+    if (threadIdx.x == 0 && ck + 1 < K) {
+      const int j = ck + 1;
+      const int pos = __hip_atomic_fetch_add(resv + j, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (pos < q.BX) {
+        __hip_atomic_store(ring + (long long)j * q.BX + pos, cb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        stores_done();
+        __hip_atomic_fetch_add(tail + j, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+  }
+}
+
+// queue (x, 0) = the set-x entries of the dispatch order (identity or the caller's
+// permutation); every other queue empty
+__global__ void nmpc_sched_init_kernel(int B, int K, const int* order, SchedQ q) {
+  const long long n = (long long)NXCD * K * q.BX;
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) {
+    const int x = (int)(i / ((long long)K * q.BX));
+    const long long r = i - (long long)x * K * q.BX;
+    const int j = (int)(r / q.BX), c = (int)(r - (long long)j * q.BX);
+    int v = -1;
+    const long long pos = (long long)c * NXCD + x;  // dispatch position
+    if (j == 0 && pos < B) {
+      v = order ? order[pos] : (int)pos;
+      if (v < 0 || v >= B) v = B;  // out-of-range entry: claimed, then skipped
+    }
+    q.ring[i] = v;
+  }
+  if (i < (long long)NXCD * K) {
+    const int x = (int)(i / K), j = (int)(i - (long long)x * K);
+    const int nset = (B - x + NXCD - 1) / NXCD;
+    q.head[i] = 0;
+    q.tail[i] = j == 0 ? nset : 0;
+    q.resv[i] = j == 0 ? nset : 0;
+  }
+  if (i == 0) q.err[0] = 0;
 }
 
 // closed-loop shift kernel (Python/NMPC_TT.py:13-30): one thread per scenario
@@ -2786,6 +2923,7 @@ int fail(int code, const std::string& msg) {
 
 typedef void (*KernFn)(const Params*, int, IO);
 typedef void (*LoopFn)(const Params*, int, IO, Loop);
+typedef void (*SchedFn)(const Params*, int, IO, Loop, SchedQ);
 
 struct nmpc_handle {
   Params hp;
@@ -2799,6 +2937,12 @@ struct nmpc_handle {
   size_t ibuf_bytes = 0;
   KernFn kern = nullptr;
   LoopFn loop = nullptr;
+  SchedFn sched = nullptr;
+  int resident = 0;            // closed-loop waves resident at once (occupancy x CUs)
+  int* dsched = nullptr;       // step-queue scheduler state
+  size_t sched_bytes = 0;
+  int last_policy = 0;         // last closed-loop launch: 0 one workgroup per scenario, 1 step queues
+  int* last_err = nullptr;     // device flag of the last step-queue launch
   int ws_doubles = 0;
   bool trace = false;
   double* dtrace = nullptr;
@@ -2813,15 +2957,15 @@ using CapB = Cap<31, 21>;
 using CapC = Cap<63, 21>;   // any supported shape
 
 template <class CAP>
-static void set_class(KernFn* fn, LoopFn* lfn, int* lds_doubles, int* ws_doubles) {
-  *fn = nmpc_solve_kernel<CAP>; *lfn = nmpc_closed_loop_kernel<CAP>;
+static void set_class(KernFn* fn, LoopFn* lfn, SchedFn* sfn, int* lds_doubles, int* ws_doubles) {
+  *fn = nmpc_solve_kernel<CAP>; *lfn = nmpc_closed_loop_kernel<CAP>; *sfn = nmpc_closed_loop_sched_kernel<CAP>;
   *lds_doubles = CAP::L.total; *ws_doubles = CAP::L.wstotal;
 }
 
-static void pick_class(const Params& P, KernFn* fn, LoopFn* lfn, int* lds_doubles, int* ws_doubles) {
-  if (P.N <= CapA::nmax && P.m <= CapA::mmax) set_class<CapA>(fn, lfn, lds_doubles, ws_doubles);
-  else if (P.N <= CapB::nmax && P.m <= CapB::mmax) set_class<CapB>(fn, lfn, lds_doubles, ws_doubles);
-  else set_class<CapC>(fn, lfn, lds_doubles, ws_doubles);
+static void pick_class(const Params& P, KernFn* fn, LoopFn* lfn, SchedFn* sfn, int* lds_doubles, int* ws_doubles) {
+  if (P.N <= CapA::nmax && P.m <= CapA::mmax) set_class<CapA>(fn, lfn, sfn, lds_doubles, ws_doubles);
+  else if (P.N <= CapB::nmax && P.m <= CapB::mmax) set_class<CapB>(fn, lfn, sfn, lds_doubles, ws_doubles);
+  else set_class<CapC>(fn, lfn, sfn, lds_doubles, ws_doubles);
 }
 
 static int ensure_ws(nmpc_handle* h, int B) {
@@ -2905,7 +3049,7 @@ int nmpc_create(const nmpc_desc* desc, nmpc_handle** out) {
   P.o = desc->opts;
   {
     int ldsd = 0;
-    pick_class(P, &h->kern, &h->loop, &ldsd, &h->ws_doubles);
+    pick_class(P, &h->kern, &h->loop, &h->sched, &ldsd, &h->ws_doubles);
     h->lds_bytes = ldsd * 8;
   }
   if (const char* e = std::getenv("NMPC_LDS_BYTES")) {  // diagnostics: pad LDS to cap workgroups per CU
@@ -2924,10 +3068,25 @@ int nmpc_create(const nmpc_desc* desc, nmpc_handle** out) {
   if (hipFuncSetAttribute((const void*)h->kern, hipFuncAttributeMaxDynamicSharedMemorySize,
                           h->lds_bytes) != hipSuccess ||
       hipFuncSetAttribute((const void*)h->loop, hipFuncAttributeMaxDynamicSharedMemorySize,
+                          h->lds_bytes) != hipSuccess ||
+      hipFuncSetAttribute((const void*)h->sched, hipFuncAttributeMaxDynamicSharedMemorySize,
                           h->lds_bytes) != hipSuccess) {
     hipFree(h->dprm); delete h; return fail(NMPC_E_HIP, "hipFuncSetAttribute(MaxDynamicSharedMemorySize)");
   }
   *out = h;
+  return NMPC_OK;
+}
+
+int nmpc_closed_loop_info(nmpc_handle* h, int32_t* policy, int32_t* resident, int32_t* sched_err) {
+  if (!h) return fail(NMPC_E_INVALID, "null handle");
+  if (policy) *policy = h->last_policy;
+  if (resident) *resident = h->resident;
+  if (sched_err) {
+    int e = 0;
+    if (h->last_err && hipMemcpy(&e, h->last_err, sizeof(int), hipMemcpyDeviceToHost) != hipSuccess)
+      return fail(NMPC_E_HIP, "reading the scheduler flag");
+    *sched_err = e;
+  }
   return NMPC_OK;
 }
 
@@ -2938,6 +3097,7 @@ int nmpc_destroy(nmpc_handle* h) {
   if (h->ibuf) hipFree(h->ibuf);
   if (h->dtrace) hipFree(h->dtrace);
   if (h->dws) hipFree(h->dws);
+  if (h->dsched) hipFree(h->dsched);
   delete h;
   return NMPC_OK;
 }
@@ -3126,8 +3286,46 @@ int nmpc_closed_loop_dev(nmpc_handle* h, int32_t B, int32_t K, const double* lbx
   lp.pstep = p_step; lp.ld_ps = ld_ps;
   lp.st_hist = status_hist; lp.it_hist = iters_hist;
   lp.order = order;
-  hipLaunchKernelGGL(h->loop, dim3(B), dim3(WAVE), h->lds_bytes, (hipStream_t)stream,
-                     (const Params*)h->dprm, (int)B, io, lp);
+  // more scenarios than resident waves: the step-queue scheduler (persistent waves,
+  // lowest step first), unless NMPC_CLOSED_LOOP=static (diagnostics: one workgroup per
+  // scenario in dispatch order)
+  if (h->resident == 0) {
+    int per_cu = 0, cus = 0;
+    hipDeviceProp_t prop;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)h->sched, WAVE, h->lds_bytes) != hipSuccess ||
+        hipGetDeviceProperties(&prop, h->device) != hipSuccess)
+      return fail(NMPC_E_HIP, "occupancy query");
+    cus = prop.multiProcessorCount;
+    h->resident = per_cu * cus;
+  }
+  const char* pol = std::getenv("NMPC_CLOSED_LOOP");
+  const bool use_q = (B > h->resident) && h->resident >= NXCD && !(pol && std::strcmp(pol, "static") == 0);
+  if (use_q) {
+    const int BX = (B + NXCD - 1) / NXCD;
+    const size_t nint = (size_t)3 * NXCD * K + (size_t)NXCD * K * BX + 1;
+    if (nint * sizeof(int) > h->sched_bytes) {
+      if (h->dsched) hipFree(h->dsched);
+      h->dsched = nullptr; h->sched_bytes = 0;
+      if (hipMalloc(&h->dsched, nint * sizeof(int)) != hipSuccess) return fail(NMPC_E_NOMEM, "hipMalloc scheduler");
+      h->sched_bytes = nint * sizeof(int);
+    }
+    SchedQ q;
+    q.head = h->dsched; q.tail = q.head + NXCD * K; q.resv = q.tail + NXCD * K;
+    q.ring = q.resv + NXCD * K; q.err = q.ring + (size_t)NXCD * K * BX; q.BX = BX;
+    const long long n = (long long)NXCD * K * BX;
+    const int thr = 256;
+    hipLaunchKernelGGL(nmpc_sched_init_kernel, dim3((unsigned)((n + thr - 1) / thr)), dim3(thr), 0,
+                       (hipStream_t)stream, (int)B, (int)K, (const int*)order, q);
+    hipLaunchKernelGGL(h->sched, dim3(h->resident), dim3(WAVE), h->lds_bytes, (hipStream_t)stream,
+                       (const Params*)h->dprm, (int)B, io, lp, q);
+    h->last_policy = 1;
+    h->last_err = q.err;
+  } else {
+    h->last_policy = 0;
+    h->last_err = nullptr;
+    hipLaunchKernelGGL(h->loop, dim3(B), dim3(WAVE), h->lds_bytes, (hipStream_t)stream,
+                       (const Params*)h->dprm, (int)B, io, lp);
+  }
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return fail(NMPC_E_HIP, std::string("closed-loop launch: ") + hipGetErrorString(e));
   return NMPC_OK;

@@ -23,7 +23,7 @@ if os.environ.get("NMPC_LIB"):
 EXPORTS = (
     "nmpc_default_options", "nmpc_create", "nmpc_destroy", "nmpc_dims",
     "nmpc_solve_batch", "nmpc_solve_batch_dev", "nmpc_set_trace", "nmpc_read_trace",
-    "nmpc_shift_dev", "nmpc_closed_loop_dev", "nmpc_last_error", "nmpc_kernel_info",
+    "nmpc_shift_dev", "nmpc_closed_loop_dev", "nmpc_closed_loop_info", "nmpc_last_error", "nmpc_kernel_info",
 )
 
 _OPT_INT = ("max_iter", "acceptable_iter", "max_soc", "max_soft_resto_iters")
@@ -100,6 +100,7 @@ def lib():
     L.nmpc_last_error.argtypes = []
     L.nmpc_last_error.restype = C.c_char_p
     L.nmpc_kernel_info.argtypes = [vp, i32p, i32p]
+    L.nmpc_closed_loop_info.argtypes = [vp, i32p, i32p, i32p]
     for n in EXPORTS:
         if n not in ("nmpc_default_options", "nmpc_last_error"):
             getattr(L, n).restype = C.c_int

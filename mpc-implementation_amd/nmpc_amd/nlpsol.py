@@ -300,6 +300,13 @@ class Solver:
         _lib.check(_lib.lib().nmpc_read_trace(self._h, B, _dptr(buf)))
         return buf
 
+    def closed_loop_info(self):
+        """Scheduling of the last closed_loop_device launch (nmpc_closed_loop_info)."""
+        pol, res, err = C.c_int32(), C.c_int32(), C.c_int32()
+        _lib.check(_lib.lib().nmpc_closed_loop_info(self._h, C.byref(pol), C.byref(res), C.byref(err)))
+        return {"policy": ("step_queues" if pol.value == 1 else "per_scenario"), "resident_waves": res.value,
+                "scheduler_error": err.value}
+
     def kernel_info(self):
         lds, tps = C.c_int32(), C.c_int32()
         _lib.check(_lib.lib().nmpc_kernel_info(self._h, C.byref(lds), C.byref(tps)))

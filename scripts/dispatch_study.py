@@ -7,7 +7,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "mpc-implementation_amd"))
 from nmpc_amd import nlpsol, config_spec, draw_scenarios, REFERENCE_OPTS
 from nmpc_amd.schedule import longest_first
-K, W, B = 20, 2, int(sys.argv[1]) if len(sys.argv) > 1 else 4096
+K, B = 20, int(sys.argv[1]) if len(sys.argv) > 1 else 4096
+W = int(sys.argv[2]) if len(sys.argv) > 2 else 2
 spec = config_spec(3)
 s = nlpsol("solver", "ipopt", spec, REFERENCE_OPTS)
 f64 = dict(dtype=torch.float64, device="cuda")

@@ -375,6 +375,56 @@ def test_closed_loop_dispatch_order_does_not_change_results():
     np.testing.assert_array_equal(got["iters"][:, 3:], ref["iters"][:, 3:])
 
 
+def test_closed_loop_step_queues_match_per_scenario_dispatch():
+    """More scenarios than resident waves: nmpc_closed_loop_dev runs the step-queue
+    scheduler (persistent waves claim (scenario, step) pairs, lowest step first, each
+    scenario pinned to one XCD).  Results are bitwise those of one workgroup per
+    scenario (NMPC_CLOSED_LOOP=static), with and without a dispatch order, and no wave
+    reports a scheduler wait error."""
+    import torch
+    from nmpc_amd import make_spec
+
+    spec = make_spec("race_track_2", N=20, T=0.2)
+    s = _solver(spec)
+    f64 = dict(dtype=torch.float64, device="cuda")
+    K = 3
+    # learn the resident-wave count with a small launch, then exceed it
+    P0, bnd, vt0, wt0 = _closed_loop_inputs(spec, 8, 5)
+    s.closed_loop_device(1, *bnd, torch.tensor(P0, **f64), torch.zeros(8, spec.nw, **f64), vt0, wt0)
+    torch.cuda.synchronize()
+    res = s.closed_loop_info()["resident_waves"]
+    assert res >= 8
+    B = res + 173
+    P, bnd, vt, wt = _closed_loop_inputs(spec, B, 1003)
+
+    def run(order=None):
+        p = torch.tensor(P, **f64)
+        w = torch.zeros(B, spec.nw, **f64)
+        hist = {"u": torch.empty(K, B, 6, **f64), "x": torch.empty(K, B, 8, **f64), "f": torch.empty(K, B, **f64),
+                "fov": torch.empty(K, B, **f64),
+                "status": torch.full((K, B), 99, dtype=torch.int32, device="cuda"),
+                "iters": torch.full((K, B), -1, dtype=torch.int32, device="cuda")}
+        s.closed_loop_device(K, *bnd, p, w, vt, wt, hist, order=order)
+        torch.cuda.synchronize()
+        return {k: v.cpu().numpy() for k, v in hist.items()}, p.cpu().numpy(), w.cpu().numpy()
+
+    os.environ["NMPC_CLOSED_LOOP"] = "static"
+    try:
+        ref, p_ref, w_ref = run()
+        assert s.closed_loop_info()["policy"] == "per_scenario"
+    finally:
+        del os.environ["NMPC_CLOSED_LOOP"]
+    g = torch.Generator().manual_seed(9)
+    for order in (None, torch.randperm(B, generator=g).to(torch.int32).cuda()):
+        got, p_got, w_got = run(order)
+        info = s.closed_loop_info()
+        assert info["policy"] == "step_queues" and info["scheduler_error"] == 0, info
+        for k in ref:
+            np.testing.assert_array_equal(got[k], ref[k], err_msg=k)
+        np.testing.assert_array_equal(p_got, p_ref)
+        np.testing.assert_array_equal(w_got, w_ref)
+
+
 def test_closed_loop_parity_with_oracle_loop():
     """The fused closed loop against the oracle's own solve + shift_timestep loop
     (Python/NMPC_TT.py:348-402 restated) under a target schedule that changes
