@@ -74,8 +74,10 @@ def pmc_traffic(kernel, steps, batch):
 
 
 def _cpu_worker(args):
-    """Solve scenarios rows[i::nproc] cold (u=0) with the oracle until the budget runs out."""
-    i, nproc, layout, N, T, P, lbx, ubx, lbg, ubg, budget_s, model = args
+    """The bench's closed loop on the CPU oracle for scenarios rows[i::nproc]: each
+    scenario runs K warm-started MPC steps (solve, then shift_timestep with the GPU
+    line's target controls, Python/NMPC_TT.py:13-30,348-402) until the budget runs out."""
+    i, nproc, layout, N, T, P, lbx, ubx, lbg, ubg, budget_s, model, K = args
     import warnings
     from threadpoolctl import threadpool_limits
 
@@ -84,23 +86,32 @@ def _cpu_worker(args):
     sys.path.insert(0, ROOT)
     from oracle import nmpc_oracle as orc
 
-    solver = orc.IpoptDense(orc.make_problem(layout, N=N, T=T, model=model), orc.REFERENCE_OPTS)
+    prob = orc.make_problem(layout, N=N, T=T, model=model)
+    solver = orc.IpoptDense(prob, orc.REFERENCE_OPTS)
+    nx, nu = prob.nx, prob.nu
     t0 = time.perf_counter()
-    n = iters = 0
+    times, iters, stats = [], [], []
     for row in range(i, P.shape[0], nproc):
-        if time.perf_counter() - t0 >= budget_s:
-            break
-        r = solver.solve(np.zeros(len(lbx)), lbx, ubx, lbg, ubg, P[row])
-        iters += r["iter"]
-        n += 1
-    return n, iters, time.perf_counter() - t0
+        x0, xs, u0 = P[row, :nx].copy(), P[row, nx:nx + 3].copy(), np.zeros(len(lbx))
+        for _ in range(K):
+            if time.perf_counter() - t0 >= budget_s:
+                return times, iters, stats
+            t1 = time.perf_counter()
+            r = solver.solve(u0, lbx, ubx, lbg, ubg, np.concatenate([x0, xs, P[row, nx + 3:]]))
+            times.append(time.perf_counter() - t1)
+            iters.append(r["iter"])
+            stats.append(r["status"])
+            x0, u1, xs = orc.shift_timestep(prob, x0, r["x"].reshape(N, nu).T, xs, con_t=(12.0, 0.01))
+            u0 = u1.T.ravel()
+    return times, iters, stats
 
 
-def cpu_baseline(spec_cfg, P, lbx, ubx, lbg, ubg, budget_s=15.0):
-    """Time the CPU oracle (numpy dense IPOPT restatement, oracle/nmpc_oracle.py)
-    on a bounded sample of the same scenarios (cold start), one scenario per
-    worker process at a time (scenarios split across processes).
-    Must run before this process touches the GPU (the workers are forked)."""
+def cpu_baseline(spec_cfg, cfg, P, lbx, ubx, lbg, ubg, K, budget_s=15.0):
+    """Time the CPU oracle (numpy dense IPOPT restatement, oracle/nmpc_oracle.py) on a
+    bounded sample of the bench's own workload: the same scenarios through the same
+    warm-started closed loop (solve + shift), one scenario per worker process at a time
+    (scenarios split across processes).  Must run before this process
+    touches the GPU (the workers are forked)."""
     import multiprocessing as mp
 
     try:
@@ -109,18 +120,24 @@ def cpu_baseline(spec_cfg, P, lbx, ubx, lbg, ubg, budget_s=15.0):
         ncpu = os.cpu_count() or 1
     nproc = max(1, min(16, ncpu))  # the GPU box's CPU share is 16
     layout = "race_track_2" if spec_cfg.n_obs == 10 else (None if spec_cfg.n_obs == 0 else "nmpc_tt")
-    sample = P[: nproc * 256]
+    sample = P[: nproc * 64]
     t0 = time.perf_counter()
     with mp.get_context("fork").Pool(nproc) as pool:
         res = pool.map(_cpu_worker, [(i, nproc, layout, spec_cfg.N, spec_cfg.T, sample, lbx, ubx, lbg, ubg,
-                                      budget_s, spec_cfg.model) for i in range(nproc)])
+                                      budget_s, spec_cfg.model, K) for i in range(nproc)])
     wall = time.perf_counter() - t0
-    n = sum(r[0] for r in res)
-    iters = sum(r[1] for r in res)
+    times = np.concatenate([np.asarray(r[0], dtype=float) for r in res])
+    iters = np.concatenate([np.asarray(r[1], dtype=float) for r in res])
+    sts = np.concatenate([np.asarray(r[2], dtype=int) for r in res])
+    n = len(times)
     return {"value": n / wall, "unit": "MPC steps/s", "cores": nproc, "kind": "port",
-            "sample": f"{n} cold-start solves (u=0) of config-{3 if spec_cfg.n_obs == 10 else '?'} scenarios by "
-                      f"oracle/nmpc_oracle.py (numpy dense single-shooting IPOPT restatement), {nproc} worker "
-                      f"processes x ~{budget_s:.0f}s, wall {wall:.1f}s, mean {iters / max(n, 1):.1f} iterations"}
+            "sample": f"{n} warm-started closed-loop MPC steps (solve + shift, up to {K} per scenario) of "
+                      f"config-{cfg} scenarios by oracle/nmpc_oracle.py (numpy dense single-shooting IPOPT "
+                      f"restatement), {nproc} worker processes x ~{budget_s:.0f}s, wall {wall:.1f}s",
+            "mean_ip_iterations": float(iters.mean()) if n else None,
+            "solve_ms_p50": float(np.percentile(times, 50) * 1e3) if n else None,
+            "solve_ms_p99": float(np.percentile(times, 99) * 1e3) if n else None,
+            "status_histogram": {int(k): int(v) for k, v in zip(*np.unique(sts, return_counts=True))}}
 
 
 def main():
@@ -155,7 +172,7 @@ def main():
     cpu_res = None
     if world == 1 and not args.no_cpu_baseline:  # forks workers: before the GPU is initialised
         lb = spec.bounds()
-        cpu_res = cpu_baseline(spec, draw_scenarios(spec, B, seed=1000 + args.config), *lb,
+        cpu_res = cpu_baseline(spec, args.config, draw_scenarios(spec, B, seed=1000 + args.config), *lb, K,
                                budget_s=args.cpu_budget)
     # NMPC_BENCH_BACKEND=gloo rehearses the multi-rank path on one GPU (all ranks on
     # cuda:0); the measured configuration is one process per GPU over RCCL ("nccl")
@@ -283,6 +300,8 @@ def main():
         kern_avg_s = float(np.mean(kern_ms)) / 1e3
         steps_per_launch = K if args.mode == "fused" else 1
         kname = "nmpc_closed_loop_kernel" if args.mode == "fused" else "nmpc_solve_kernel"
+        if args.mode == "fused" and solver.closed_loop_info()["policy"] == "step_queues":
+            kname = "nmpc_closed_loop_sched_kernel"
         flops_launch = B * steps_per_launch * ibar * (spec.N + 1) * KFLOP_PER_STAGE_ITER * 1e3
         achieved_tf = flops_launch / kern_avg_s / 1e12
         bps, s_stage, b_iter, io = survey_bytes_per_step(spec, ibar)
@@ -318,9 +337,17 @@ def main():
             "status_histogram": status_hist,
         }
         if args.mode == "fused":
-            res["dispatch"] = ("index order" if (args.in_order or W == 0) else
-                               "longest-expected-first: scenarios sorted by the iterations of the "
-                               f"{W} warm-up MPC steps that precede the timed steps (nmpc_amd.schedule)")
+            info = solver.closed_loop_info()
+            first = ("index order" if (args.in_order or W == 0) else
+                     "longest-expected-first by the iterations of the "
+                     f"{W} warm-up MPC steps that precede the timed steps (nmpc_amd.schedule)")
+            if info["policy"] == "step_queues":
+                res["dispatch"] = (f"step queues: {info['resident_waves']} persistent waves claim (scenario, step) "
+                                   f"pairs whose previous step is done, lowest step first, scenarios pinned to an "
+                                   f"XCD; initial order {first}")
+            else:
+                res["dispatch"] = f"one workgroup per scenario, {first}"
+            res["scheduler_error"] = info["scheduler_error"]
         if fov_mean is not None:
             res["closed_loop_fov_error_mean_m"] = fov_mean  # Python/NMPC_TT.py:433-437 metric, per step
         if side is not None:
