@@ -1222,11 +1222,14 @@ struct Solver {
   __device__ __forceinline__ double resto_pn_terms(const GLB double* Us, double a, const GLB double* dps,
                                                    const GLB double* dns) const {
     double pn = 0.0, lg = 0.0, prox = 0.0;
-    for (int r = lanef(); r < ng; r += WAVE) {
+    rows([&](int r, bool on) {
       const double pv = dps ? pR[r] + a * dps[r] : pR[r], nv = dns ? nR[r] + a * dns[r] : nR[r];
-      pn += pv + nv;
-      lg += log(pv) + log(nv);
-    }
+      const double l2 = log(pv) + log(nv);
+      if (on) {
+        pn += pv + nv;
+        lg += l2;
+      }
+    });
     for (int i = lanef(); i < nw; i += WAVE) {
       const double dd = Us[i] - UR[i];
       prox += dr2(i) * dd * dd;
@@ -1244,11 +1247,14 @@ struct Solver {
     fo = df * eval_fg(Xt, dt, dc);
     double th = 0.0;
     bool bad = false;
-    for (int r = lanef(); r < ng; r += WAVE) {
+    rows([&](int r, bool on) {
       const double sv = s[r] + a * dss[r], pv = pR[r] + a * dps[r], nv = nR[r] + a * dns[r];
-      th += fabs(dt[r] - sv - pv + nv);
-      if (!isfinite(dt[r])) bad = true;
-    }
+      const double dtr = dt[r];
+      if (on) {
+        th += fabs(dtr - sv - pv + nv);
+        if (!isfinite(dtr)) bad = true;
+      }
+    });
     tht = wsum(th);
     if (wany(bad)) return false;
     phit = barrier_obj(0.0, Ut, s, dss, a) + resto_pn_terms(Ut, a, dps, dns);
@@ -1258,23 +1264,26 @@ struct Solver {
                                                         const GLB double* dps, const GLB double* dns) const {
     double a = frac_to_bound(tau_, dUs, dss);
     double b = 1.0;
-    for (int r = lanef(); r < ng; r += WAVE) {
-      if (dps[r] < 0) b = fmin(b, (-tau_ * pR[r]) / dps[r]);
-      if (dns[r] < 0) b = fmin(b, (-tau_ * nR[r]) / dns[r]);
-    }
+    rows([&](int r, bool on) {
+      const double dp = dps[r], dn = dns[r], pr = pR[r], nr = nR[r];
+      const double bp = (-tau_ * pr) / dp, bn = (-tau_ * nr) / dn;
+      if (on && dp < 0) b = fmin(b, bp);
+      if (on && dn < 0) b = fmin(b, bn);
+    });
     return fmin(a, wmin(b));
   }
   __device__ __forceinline__ double dual_frac_to_bound_resto(double tau_, const GLB double* dUs, const GLB double* dss,
                                                              const GLB double* dps, const GLB double* dns) const {
     double a = dual_frac_to_bound(tau_, dUs, dss);
     double b = 1.0;
-    for (int r = lanef(); r < ng; r += WAVE) {
-      const double pr = pR[r], nr = nR[r];
-      const double dzp = mu / pr - zpR[r] - (zpR[r] / pr) * dps[r];
-      const double dzn = mu / nr - znR[r] - (znR[r] / nr) * dns[r];
-      if (dzp < 0) b = fmin(b, (-tau_ * zpR[r]) / dzp);
-      if (dzn < 0) b = fmin(b, (-tau_ * znR[r]) / dzn);
-    }
+    rows([&](int r, bool on) {
+      const double pr = pR[r], nr = nR[r], zp = zpR[r], zn = znR[r], dp = dps[r], dn = dns[r];
+      const double dzp = mu / pr - zp - (zp / pr) * dp;
+      const double dzn = mu / nr - zn - (zn / nr) * dn;
+      const double bp = (-tau_ * zp) / dzp, bn = (-tau_ * zn) / dzn;
+      if (on && dzp < 0) b = fmin(b, bp);
+      if (on && dzn < 0) b = fmin(b, bn);
+    });
     return fmin(a, wmin(b));
   }
 
@@ -1417,11 +1426,13 @@ struct Solver {
     ft = df * eval_fg(Xt, dt, dc);
     double th = 0.0;
     bool bad = false;
-    for (int r = lanef(); r < ng; r += WAVE) {
-      const double sv = s[r] + a * dss[r];
-      th += fabs(dt[r] - sv);
-      if (!isfinite(dt[r])) bad = true;
-    }
+    rows([&](int r, bool on) {
+      const double sv = s[r] + a * dss[r], dtr = dt[r];
+      if (on) {
+        th += fabs(dtr - sv);
+        if (!isfinite(dtr)) bad = true;
+      }
+    });
     tht = wsum(th);
     bad = wany(bad) || !isfinite(ft);
     if (bad) return false;
@@ -1545,7 +1556,10 @@ __device__ __forceinline__ void resto_phase(const Params* __restrict__ prm, doub
         // ---- progress w.r.t. the original problem (RestoConvergenceCheck)
         if (!firstR) {
           double tho = 0.0;
-          for (int r = S.lanef(); r < ng; r += WAVE) tho += fabs(S.d[r] - S.s[r]);
+          S.rows([&](int r, bool on) {
+            const double t = fabs(S.d[r] - S.s[r]);
+            if (on) tho += t;
+          });
           tho = wsum(tho);
           S.mu = V[0];
           const double pho = S.barrier_obj(V[12], S.U, S.s, nullptr, 0.0);
@@ -1577,30 +1591,31 @@ __device__ __forceinline__ void resto_phase(const Params* __restrict__ prm, doub
           sumz += fabs(S.zl[i]) + fabs(S.zu[i]);
           frx += S.dr2(i) * dd * dd;
         }
-        for (int r = S.lanef(); r < ng; r += WAVE) {
-          const double yr = S.y[r], pr = S.pR[r], nr = S.nR[r];
-          dinf = fmax(dinf, fmax(fabs(-yr - S.vl[r] + S.vu[r]), fmax(fabs(rho - yr - S.zpR[r]), fabs(rho + yr - S.znR[r]))));
-          const double drr = S.d[r] - pr + nr;
+        S.rows([&](int r, bool on) {
+          const double yr = S.y[r], pr = S.pR[r], nr = S.nR[r], vlr = S.vl[r], vur = S.vu[r];
+          const double zp = S.zpR[r], zn = S.znR[r], dr = S.d[r], sr = S.s[r], dcr = S.dc[r];
+          const double lo = S.dl[r], hi = S.du[r];
+          const bool hl = S.hasl(lo), hu = S.hasu(hi);
+          const double di = fmax(fabs(-yr - vlr + vur), fmax(fabs(rho - yr - zp), fabs(rho + yr - zn)));
+          const double drr = dr - pr + nr;
           double c1 = 0.0, c2 = 0.0;
-          if (S.hasl(S.dl[r])) {
-            c1 = fmax(c1, S.dl[r] - drr);
-            cmr = fmax(cmr, fabs((S.s[r] - S.dl[r]) * S.vl[r]));
-            c2 = fmax(c2, S.dl[r] - S.d[r]);
+          if (hl) { c1 = fmax(c1, lo - drr); c2 = fmax(c2, lo - dr); }
+          if (hu) { c1 = fmax(c1, drr - hi); c2 = fmax(c2, dr - hi); }
+          const double cl = fabs((sr - lo) * vlr), cu = fabs((hi - sr) * vur), uc = c2 / dcr;
+          if (on) {  // max reductions are order-free; sums keep the per-lane row order
+            dinf = fmax(dinf, di);
+            if (hl) cmr = fmax(cmr, cl);
+            if (hu) cmr = fmax(cmr, cu);
+            cmr = fmax(cmr, fmax(fabs(pr * zp), fabs(nr * zn)));
+            cv = fmax(cv, c1);
+            ucv = fmax(ucv, uc);
+            sumy += fabs(yr);
+            sumv += fabs(vlr) + fabs(vur);
+            sump += fabs(zp) + fabs(zn);
+            frp += pr + nr;
+            if (!isfinite(dr)) bad = true;
           }
-          if (S.hasu(S.du[r])) {
-            c1 = fmax(c1, drr - S.du[r]);
-            cmr = fmax(cmr, fabs((S.du[r] - S.s[r]) * S.vu[r]));
-            c2 = fmax(c2, S.d[r] - S.du[r]);
-          }
-          cmr = fmax(cmr, fmax(fabs(pr * S.zpR[r]), fabs(nr * S.znR[r])));
-          cv = fmax(cv, c1);
-          ucv = fmax(ucv, c2 / S.dc[r]);
-          sumy += fabs(yr);
-          sumv += fabs(S.vl[r]) + fabs(S.vu[r]);
-          sump += fabs(S.zpR[r]) + fabs(S.znR[r]);
-          frp += pr + nr;
-          if (!isfinite(S.d[r])) bad = true;
-        }
+        });
         dinf = wmax(dinf); cv = wmax(cv); cmr = wmax(cmr); ucv = wmax(ucv);
         sumy = wsum(sumy); sumz = wsum(sumz); sumv = wsum(sumv); sump = wsum(sump);
         frp = wsum(frp); frx = wsum(frx);
@@ -1633,15 +1648,21 @@ __device__ __forceinline__ void resto_phase(const Params* __restrict__ prm, doub
               if (S.hasl(S.xl[i])) cm = fmax(cm, fabs((S.U[i] - S.xl[i]) * S.zl[i] - mu_));
               if (S.hasu(S.xu[i])) cm = fmax(cm, fabs((S.xu[i] - S.U[i]) * S.zu[i] - mu_));
             }
-            for (int r = S.lanef(); r < ng; r += WAVE) {
-              const double yr = S.y[r];
-              dn = fmax(dn, fmax(fabs(-yr - S.vl[r] + S.vu[r]),
-                                 fmax(fabs(rho - yr - S.zpR[r]), fabs(rho + yr - S.znR[r]))));
-              if (S.hasl(S.dl[r])) cm = fmax(cm, fabs((S.s[r] - S.dl[r]) * S.vl[r] - mu_));
-              if (S.hasu(S.du[r])) cm = fmax(cm, fabs((S.du[r] - S.s[r]) * S.vu[r] - mu_));
-              cm = fmax(cm, fmax(fabs(S.pR[r] * S.zpR[r] - mu_), fabs(S.nR[r] * S.znR[r] - mu_)));
-              pinf = fmax(pinf, fabs(S.d[r] - S.s[r] - S.pR[r] + S.nR[r]));
-            }
+            S.rows([&](int r, bool on) {
+              const double yr = S.y[r], vlr = S.vl[r], vur = S.vu[r], zp = S.zpR[r], zn = S.znR[r];
+              const double sr = S.s[r], dr = S.d[r], pr = S.pR[r], nr = S.nR[r], lo = S.dl[r], hi = S.du[r];
+              const double dv = fmax(fabs(-yr - vlr + vur), fmax(fabs(rho - yr - zp), fabs(rho + yr - zn)));
+              const double cl = fabs((sr - lo) * vlr - mu_), cu = fabs((hi - sr) * vur - mu_);
+              const double cp = fmax(fabs(pr * zp - mu_), fabs(nr * zn - mu_));
+              const double pi = fabs(dr - sr - pr + nr);
+              if (on) {
+                dn = fmax(dn, dv);
+                if (S.hasl(lo)) cm = fmax(cm, cl);
+                if (S.hasu(hi)) cm = fmax(cm, cu);
+                cm = fmax(cm, cp);
+                pinf = fmax(pinf, pi);
+              }
+            });
             return fmax(fmax(wmax(dn) / V[13], wmax(pinf)), wmax(cm) / V[14]);
           };
           double se = sub_errR(V[4]);
@@ -1799,27 +1820,35 @@ __device__ __forceinline__ void resto_phase(const Params* __restrict__ prm, doub
             else nzu = 0.0;
             S.zl[i] = nzl; S.zu[i] = nzu;
           }
-          for (int r = S.lanef(); r < ng; r += WAVE) {
-            double dvl, dvu;
-            S.dv_s(r, dsa[r], dvl, dvu);
-            const double pr = S.pR[r], nr = S.nR[r];
-            const double dzp = V[4] / pr - S.zpR[r] - (S.zpR[r] / pr) * dpa[r];
-            const double dzn = V[4] / nr - S.znR[r] - (S.znR[r] / nr) * dna[r];
-            const double sn = S.s[r] + V[19] * dsa[r];
-            const double pn = pr + V[19] * dpa[r], nn = nr + V[19] * dna[r];
-            double nvl = S.vl[r] + ad * dvl, nvu = S.vu[r] + ad * dvu;
-            if (S.hasl(S.dl[r])) { const double Sn = sn - S.dl[r]; nvl = fmax(fmin(nvl, ks * V[4] / Sn), V[4] / (ks * Sn)); }
+          const double muR = V[4], aP = V[19];  // volatile LDS scalars read once
+          S.rows([&](int r, bool on) {
+            const double sr = S.s[r], lo = S.dl[r], hi = S.du[r], vlr = S.vl[r], vur = S.vu[r];
+            const double dsr = dsa[r], dpr = dpa[r], dnr = dna[r], dyr = dya[r];
+            const double pr = S.pR[r], nr = S.nR[r], zp = S.zpR[r], zn = S.znR[r], yr = S.y[r], dtr = S.dt[r];
+            const bool hl = S.hasl(lo), hu = S.hasu(hi);
+            double dvl = 0.0, dvu = 0.0;  // dv_s with the loads hoisted
+            if (hl) { const double iS = rcp(sr - lo); dvl = S.mu * iS - vlr - vlr * iS * dsr; }
+            if (hu) { const double iS = rcp(hi - sr); dvu = S.mu * iS - vur + vur * iS * dsr; }
+            const double dzp = muR / pr - zp - (zp / pr) * dpr;
+            const double dzn = muR / nr - zn - (zn / nr) * dnr;
+            const double sn = sr + aP * dsr;
+            const double pn = pr + aP * dpr, nn = nr + aP * dnr;
+            double nvl = vlr + ad * dvl, nvu = vur + ad * dvu;
+            if (hl) { const double Sn = sn - lo; nvl = fmax(fmin(nvl, ks * muR / Sn), muR / (ks * Sn)); }
             else nvl = 0.0;
-            if (S.hasu(S.du[r])) { const double Sn = S.du[r] - sn; nvu = fmax(fmin(nvu, ks * V[4] / Sn), V[4] / (ks * Sn)); }
+            if (hu) { const double Sn = hi - sn; nvu = fmax(fmin(nvu, ks * muR / Sn), muR / (ks * Sn)); }
             else nvu = 0.0;
-            const double nzp = S.zpR[r] + ad * dzp, nzn = S.znR[r] + ad * dzn;
-            S.zpR[r] = fmax(fmin(nzp, ks * V[4] / pn), V[4] / (ks * pn));
-            S.znR[r] = fmax(fmin(nzn, ks * V[4] / nn), V[4] / (ks * nn));
-            S.y[r] = S.y[r] + V[19] * dya[r];
-            S.vl[r] = nvl; S.vu[r] = nvu;
-            S.s[r] = sn; S.pR[r] = pn; S.nR[r] = nn;
-            S.d[r] = S.dt[r];
-          }
+            const double nzp = zp + ad * dzp, nzn = zn + ad * dzn;
+            const double zpn = fmax(fmin(nzp, ks * muR / pn), muR / (ks * pn));
+            const double znn = fmax(fmin(nzn, ks * muR / nn), muR / (ks * nn));
+            if (on) {
+              S.zpR[r] = zpn; S.znR[r] = znn;
+              S.y[r] = yr + aP * dyr;
+              S.vl[r] = nvl; S.vu[r] = nvu;
+              S.s[r] = sn; S.pR[r] = pn; S.nR[r] = nn;
+              S.d[r] = dtr;
+            }
+          });
           for (int i = S.lanef(); i < nw; i += WAVE) S.U[i] = S.Ut[i];
           if (S.lanef() <= N) {
 #pragma unroll
