@@ -2789,9 +2789,11 @@ __global__ __launch_bounds__(WAVE, NMPC_WAVES_PER_EU) void nmpc_closed_loop_kern
 //    a scenario's state (p, w, histories) is only ever handed between waves sharing
 //    an L2, through agent-scope release / acquire fences.
 //  * Claims and publishes are agent-scope atomics by lane 0.
-//  * Exit: a wave leaves once every queue of its set is fully claimed.  A claimed slot
-//    always has a running writer, so waiting on it is short; a wave that waits longer
-//    than kSchedWaitTicks anyway sets err and leaves instead of spinning forever.
+//  * Exit: a wave leaves as soon as nothing in its set is claimable: every unfinished
+//    scenario is then running on some wave, and each publisher claims again right
+//    after publishing, so no published step is left without a live wave and no wave
+//    spins.  A claimed slot always has a running writer, so waiting for its store is
+//    short; a wave that waits longer than kSchedWaitTicks anyway sets err and leaves.
 constexpr int NXCD = 8;  // MI355X: 8 XCDs
 struct SchedQ {
   int* head;  // NXCD x K: claimed count of queue (x, j)
@@ -2801,7 +2803,7 @@ struct SchedQ {
   int* err;   // 1: a wave gave up waiting
   int BX;     // ring capacity per queue = ceil(B / NXCD)
 };
-constexpr unsigned long long kSchedWaitTicks = 6000000000ull;  // s_memrealtime (100 MHz): 60 s
+constexpr unsigned long long kSchedWaitTicks = 1000000000ull;  // s_memrealtime (100 MHz): 10 s
 
 // polling loads: relaxed (no L1 invalidation per poll); the claim is followed by one
 // acquire fence.  A scenario never leaves its XCD, so its state only has to reach the
@@ -2833,39 +2835,33 @@ __global__ __launch_bounds__(WAVE, NMPC_WAVES_PER_EU) void nmpc_closed_loop_sche
   for (;;) {
     int cb = -1, ck = -1;
     if (threadIdx.x == 0) {
-      const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-      for (;;) {
-        bool all_claimed = true, gave_up = false;
-        for (int j = jmin; j < K; ++j) {
-          const int h = ld_acq(head + j);
-          if (h >= nset) {
-            if (j == jmin) ++jmin;
-            continue;
-          }
-          all_claimed = false;
-          if (h >= ld_acq(tail + j)) continue;  // nothing published in this queue yet
-          int e = h;
-          if (!__hip_atomic_compare_exchange_strong(head + j, &e, h + 1, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                                    __HIP_MEMORY_SCOPE_AGENT)) {
-            --j;  // lost the race for this queue: look at it again
-            continue;
-          }
-          // published count > h: slot h's writer has reserved it and stores it next
-          int v = ld_acq(ring + (long long)j * q.BX + h);
-          while (v < 0 && __builtin_amdgcn_s_memrealtime() - t0 < kSchedWaitTicks) {
-            __builtin_amdgcn_s_sleep(2);
-            v = ld_acq(ring + (long long)j * q.BX + h);
-          }
-          if (v < 0) gave_up = true;
-          else { cb = v; ck = j; }
-          break;
+      // One pass over the set's queues, lowest step first.  Finding nothing to claim
+      // means every unfinished scenario of the set is running on some wave, so this
+      // wave is surplus from now on (the unfinished count only shrinks, and every
+      // publisher claims again right after publishing): it exits instead of spinning.
+      for (int j = jmin; j < K; ++j) {
+        const int h = ld_acq(head + j);
+        if (h >= nset) {
+          if (j == jmin) ++jmin;
+          continue;
         }
-        if (ck >= 0 || all_claimed) break;
-        if (gave_up || __builtin_amdgcn_s_memrealtime() - t0 > kSchedWaitTicks) {
-          __hip_atomic_store(q.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          break;
+        if (h >= ld_acq(tail + j)) continue;  // nothing published in this queue yet
+        int e = h;
+        if (!__hip_atomic_compare_exchange_strong(head + j, &e, h + 1, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                  __HIP_MEMORY_SCOPE_AGENT)) {
+          --j;  // lost the race for this queue: look at it again
+          continue;
         }
-        __builtin_amdgcn_s_sleep(127);
+        // published count > h: slot h's writer has reserved it and stores it next
+        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+        int v = ld_acq(ring + (long long)j * q.BX + h);
+        while (v < 0 && __builtin_amdgcn_s_memrealtime() - t0 < kSchedWaitTicks) {
+          __builtin_amdgcn_s_sleep(2);
+          v = ld_acq(ring + (long long)j * q.BX + h);
+        }
+        if (v < 0) __hip_atomic_store(q.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        else { cb = v; ck = j; }
+        break;
       }
     }
     cb = __builtin_amdgcn_readfirstlane(cb);
