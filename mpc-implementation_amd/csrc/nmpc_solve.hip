@@ -109,7 +109,7 @@ constexpr Lay make_layout(int N, int m) {
   L.P0 = o; o += 64; L.P1 = o; o += 64; L.pv0 = o; o += 8; L.pv1 = o; o += 8; L.St = o; o += 48;
   L.p = o; o += 64; L.ob = o; o += al2(2 * NMPC_MAX_OBS); L.inc = o; o += al2(8 * NS); L.red = o; o += 24;
   L.dl = o; o += al2(ng); L.du = o; o += al2(ng);  // row bounds (constant during a solve, read by every row pass)
-  L.rvars = o; o += 32;  // restoration-phase scalars
+  L.rvars = o; o += 40;  // line-search / restoration scalars; [32..36] barrier sums
   L.total = o;
   return L;
 }
@@ -644,9 +644,15 @@ struct Solver {
   __device__ __forceinline__ double sl_x(int i, const LDS double* u) const { return u[i] - xl[i]; }
   __device__ __forceinline__ double su_x(int i, const LDS double* u) const { return xu[i] - u[i]; }
 
-  // barrier objective phi (oracle barrier_obj) at (u, s + a*ds) [sv == null -> s]
+  // phi from the wave sums of barrier_obj (the log and damping sums do not depend on mu)
+  __device__ __forceinline__ double phi_of(double f, double logs, double damp) const {
+    return f - mu * logs + P->o.kappa_d * mu * damp;
+  }
+  // barrier objective phi (oracle barrier_obj) at (u, s + a*ds) [sv == null -> s];
+  // the sums are kept in rvars[32..33], so the accepted trial's sums serve the next
+  // iteration's reference value (same slacks bit for bit: U <- Ut, s <- s + a ds)
   __device__ __forceinline__ double barrier_obj(double f, const GLB double* u, const GLB double* sb, const GLB double* dsv,
-                                double a) const {
+                                double a) {
     STAMP0();
     double logs = 0.0, damp = 0.0;
     for (int i = lanef(); i < nw; i += WAVE) {
@@ -656,17 +662,22 @@ struct Solver {
       if (lo && !hi) damp += u[i] - xl[i];
       if (hi && !lo) damp += xu[i] - u[i];
     }
-    for (int r = lanef(); r < ng; r += WAVE) {
+    rows([&](int r, bool on) {  // both logs of a row pair in flight; sums keep the per-lane row order
+      const double lo_ = dl[r], hi_ = du[r];
       const double sv = dsv ? sb[r] + a * dsv[r] : sb[r];
-      const bool lo = hasl(dl[r]), hi = hasu(du[r]);
-      if (lo) logs += log(sv - dl[r]);
-      if (hi) logs += log(du[r] - sv);
-      if (lo && !hi) damp += sv - dl[r];
-      if (hi && !lo) damp += du[r] - sv;
-    }
+      const bool lo = hasl(lo_), hi = hasu(hi_);
+      const double ll = log(sv - lo_), lu = log(hi_ - sv);
+      if (on) {
+        if (lo) logs += ll;
+        if (hi) logs += lu;
+        if (lo && !hi) damp += sv - lo_;
+        if (hi && !lo) damp += hi_ - sv;
+      }
+    });
     logs = wsum(logs);
     damp = wsum(damp);
-    const double rr = f - mu * logs + P->o.kappa_d * mu * damp;
+    rvars[32] = logs; rvars[33] = damp;
+    const double rr = phi_of(f, logs, damp);
     STAMP1(PH_BARR);
     return rr;
   }
@@ -1187,7 +1198,7 @@ struct Solver {
                                                  GLB double* dno, GLB double* dyo, double& th, double& gsum) {
     const double kd = P->o.kappa_d;
     th = 0.0; gsum = 0.0;
-    for (int r = lanef(); r < ng; r += WAVE) {
+    rows([&](int r, bool on) {
       const int k = r / m, i = r - k * m;
       const LDS double* xk = X + k * 8;
       const LDS double* dxk = dXs + k * 8;
@@ -1202,25 +1213,32 @@ struct Solver {
       }
       double D, rs, Sp, Sn, rp, rn, Dt, Dr;
       row_resto(r, soc, D, rs, Sp, Sn, rp, rn, Dt, Dr);
-      const double c = soc ? cms[r] : d[r] - s[r] - pR[r] + nR[r];
+      const double pr = pR[r], nr = nR[r];
+      const double c = soc ? cms[r] : d[r] - s[r] - pr + nr;
       const double dyv = Dt * jd + Dr;
       const double dpv = (dyv - rp) / Sp, dnv = (-dyv - rn) / Sn;
       const double dsv = jd + c - dpv + dnv;
-      dso[r] = dsv; dpo[r] = dpv; dno[r] = dnv; dyo[r] = dyv;
+      if (on) { dso[r] = dsv; dpo[r] = dpv; dno[r] = dnv; dyo[r] = dyv; }
       if (!soc) {
-        th += fabs(c);
         const double lo = dl[r], hi = du[r], sr = s[r];
         const bool hl = hasl(lo), hu = hasu(hi);
         const double gs = -(hl ? mu / (sr - lo) : 0.0) + (hu ? mu / (hi - sr) : 0.0) +
                           kd * mu * ((hl && !hu ? 1.0 : 0.0) - (hu && !hl ? 1.0 : 0.0));
-        gsum += gs * dsv + (rho - mu / pR[r] + kd * mu) * dpv + (rho - mu / nR[r] + kd * mu) * dnv;
+        const double gr = gs * dsv + (rho - mu / pr + kd * mu) * dpv + (rho - mu / nr + kd * mu) * dnv;
+        if (on) {
+          th += fabs(c);
+          gsum += gr;
+        }
       }
-    }
+    });
     sync();
   }
   // p, n part of phi_R at s + a ds, p + a dp, n + a dn (the x/s part comes from barrier_obj)
+  __device__ __forceinline__ double pn_of(double pn, double lg, double prox) const {
+    return rho * pn + 0.5 * etaR * prox - mu * lg + P->o.kappa_d * mu * pn;
+  }
   __device__ __forceinline__ double resto_pn_terms(const GLB double* Us, double a, const GLB double* dps,
-                                                   const GLB double* dns) const {
+                                                   const GLB double* dns) {
     double pn = 0.0, lg = 0.0, prox = 0.0;
     rows([&](int r, bool on) {
       const double pv = dps ? pR[r] + a * dps[r] : pR[r], nv = dns ? nR[r] + a * dns[r] : nR[r];
@@ -1235,7 +1253,8 @@ struct Solver {
       prox += dr2(i) * dd * dd;
     }
     pn = wsum(pn); lg = wsum(lg); prox = wsum(prox);
-    return rho * pn + 0.5 * etaR * prox - mu * lg + P->o.kappa_d * mu * pn;
+    rvars[34] = pn; rvars[35] = lg; rvars[36] = prox;
+    return pn_of(pn, lg, prox);
   }
   // restoration trial point: theta_R, phi_R and the original objective fo
   __device__ __forceinline__ bool trial_resto(double a, const GLB double* dUs, const GLB double* dss,
@@ -1553,6 +1572,9 @@ __device__ __forceinline__ void resto_phase(const Params* __restrict__ prm, doub
       (void)stamps;
       while (true) {
         STAMP0();
+        // after the first restoration iteration rvars[32..36] hold the sums of the
+        // accepted trial, i.e. of the current iterate (p, n, s, U updated bit for bit)
+        const bool cachedR = !firstR;
         // ---- progress w.r.t. the original problem (RestoConvergenceCheck)
         if (!firstR) {
           double tho = 0.0;
@@ -1562,7 +1584,7 @@ __device__ __forceinline__ void resto_phase(const Params* __restrict__ prm, doub
           });
           tho = wsum(tho);
           S.mu = V[0];
-          const double pho = S.barrier_obj(V[12], S.U, S.s, nullptr, 0.0);
+          const double pho = S.phi_of(V[12], S.rvars[32], S.rvars[33]);
           S.mu = V[4];
           if (tho <= o.required_infeasibility_reduction * V[2] && isfinite(pho)) {
             const bool ok = cmp_le(tho, (1.0 - o.gamma_theta) * V[2], V[2]) ||
@@ -1723,7 +1745,8 @@ __device__ __forceinline__ void resto_phase(const Params* __restrict__ prm, doub
           V[16] = wsum(g);
           STAMP1(PH_ROWSTEP);
         }
-        V[17] = S.barrier_obj(0.0, S.U, S.s, nullptr, 0.0) + S.resto_pn_terms(S.U, 0.0, nullptr, nullptr);
+        V[17] = cachedR ? S.phi_of(0.0, S.rvars[32], S.rvars[33]) + S.pn_of(S.rvars[34], S.rvars[35], S.rvars[36])
+                        : S.barrier_obj(0.0, S.U, S.s, nullptr, 0.0) + S.resto_pn_terms(S.U, 0.0, nullptr, nullptr);
         if (V[6] < 0) {
           V[6] = o.theta_max_fact * fmax(1.0, V[15]);
           V[7] = o.theta_min_fact * fmax(1.0, V[15]);
@@ -2165,6 +2188,7 @@ __device__ __forceinline__ int solve_one(Solver<CAP>& S, const Params* __restric
   MV[0] = -1.0; MV[1] = -1.0;
   MV[2] = 0.0; MV[3] = 0.0;
   bool in_soft = false, tiny_flag = false, have_acc = false;
+  bool phic = false;  // rvars[32..33] hold the barrier sums of the current iterate (its accepted trial)
   int soft_cnt = 0, acc_cnt = 0, last_obj_iter = -1;
   MV[4] = -1e50; MV[5] = -1e50;
   const double smax = o.s_max;
@@ -2325,7 +2349,7 @@ __device__ __forceinline__ int solve_one(Solver<CAP>& S, const Params* __restric
       STAMP1(PH_LSSET);
     }
     STAMPV0(_tls);  // whole line search incl. nested phases (diagnostic slot of the old Riccati step 3)
-    const double phi_ref = S.barrier_obj(f, S.U, S.s, nullptr, 0.0);
+    const double phi_ref = phic ? S.phi_of(f, S.rvars[32], S.rvars[33]) : S.barrier_obj(f, S.U, S.s, nullptr, 0.0);
     if (MV[0] < 0) {
       MV[0] = o.theta_max_fact * fmax(1.0, theta_ref);
       MV[1] = o.theta_min_fact * fmax(1.0, theta_ref);
@@ -2585,6 +2609,7 @@ __device__ __forceinline__ int solve_one(Solver<CAP>& S, const Params* __restric
       }
       sync();
       f = f_acc;
+      phic = true;  // no barrier_obj call between the accepted trial and the next phi_ref
       STAMP1(PH_ACCEPT);
       if (!derivs_done) S.derivs(S.X, S.U);
       else {
@@ -2612,6 +2637,7 @@ __device__ __forceinline__ int solve_one(Solver<CAP>& S, const Params* __restric
   if (rio.status != 0) { status = rio.status; break; }
   f = rio.f;
   in_soft = false;
+  phic = false;
   }
 
   // ---------------- outputs (honor_original_bounds)
