@@ -434,10 +434,14 @@ struct Solver {
     if (k <= N) {
       const LDS double* xk = Xs + k * 8;
       if (k < N) f = stage_cost(xk);
-      for (int i = 0; i < m; ++i) {
-        const int r = k * m + i;
-        const double g = row_value(xk, i);
-        dst[r] = scale ? scale[r] * g : g;
+      // unrolled over the layout's row capacity: the obstacle rows' square roots overlap
+#pragma unroll
+      for (int i = 0; i < CAP::mmax; ++i) {
+        if (i < m) {
+          const int r = k * m + i;
+          const double g = row_value(xk, i);
+          dst[r] = scale ? scale[r] * g : g;
+        }
       }
     }
     sync();
