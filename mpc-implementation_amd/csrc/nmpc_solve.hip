@@ -570,9 +570,12 @@ struct Solver {
 #pragma unroll
       for (int i = 0; i < 8; ++i) w[i] = ofac * gl[k * 8 + i];
       if (yy) {
-        for (int i = 0; i < nb; ++i) {
-          const int r = k * m + i;
-          w[boxidx(i)] += dc[r] * yy[r];
+#pragma unroll
+        for (int i = 0; i < 5; ++i) {  // nb <= 5 box rows
+          if (i < nb) {
+            const int r = k * m + i;
+            w[boxidx(i)] += dc[r] * yy[r];
+          }
         }
         // compile-time bound so every row's loads issue before the first use
         double cyv[CAP::mmax - 5];
@@ -1606,6 +1609,10 @@ __device__ __forceinline__ void resto_phase(const Params* __restrict__ prm, doub
         // ---- the restoration NLP's own optimality error / termination
         S.adjoint(0.0, S.y);
         double dinf = 0, cv = 0, cmr = 0, ucv = 0, sumy = 0, sumz = 0, sumv = 0, sump = 0, frp = 0, frx = 0;
+        // the barrier error at the current mu (first sub_errR of the mu update below)
+        // from the same pass: its dual part is dinf (etaR = weight * sqrt(V[4]))
+        double cmu = 0, pinfu = 0;
+        const double muc = V[4];
         bool bad = false;
         for (int i = S.lanef(); i < nw; i += WAVE) {
           const double dd = S.U[i] - S.UR[i];
@@ -1614,6 +1621,8 @@ __device__ __forceinline__ void resto_phase(const Params* __restrict__ prm, doub
           dinf = fmax(dinf, fabs(g));
           if (S.hasl(S.xl[i])) cmr = fmax(cmr, fabs((S.U[i] - S.xl[i]) * S.zl[i]));
           if (S.hasu(S.xu[i])) cmr = fmax(cmr, fabs((S.xu[i] - S.U[i]) * S.zu[i]));
+          if (S.hasl(S.xl[i])) cmu = fmax(cmu, fabs((S.U[i] - S.xl[i]) * S.zl[i] - muc));
+          if (S.hasu(S.xu[i])) cmu = fmax(cmu, fabs((S.xu[i] - S.U[i]) * S.zu[i] - muc));
           sumz += fabs(S.zl[i]) + fabs(S.zu[i]);
           frx += S.dr2(i) * dd * dd;
         }
@@ -1628,7 +1637,14 @@ __device__ __forceinline__ void resto_phase(const Params* __restrict__ prm, doub
           if (hl) { c1 = fmax(c1, lo - drr); c2 = fmax(c2, lo - dr); }
           if (hu) { c1 = fmax(c1, drr - hi); c2 = fmax(c2, dr - hi); }
           const double cl = fabs((sr - lo) * vlr), cu = fabs((hi - sr) * vur), uc = c2 / dcr;
+          const double clm = fabs((sr - lo) * vlr - muc), cum = fabs((hi - sr) * vur - muc);
+          const double cpm = fmax(fabs(pr * zp - muc), fabs(nr * zn - muc));
+          const double pim = fabs(dr - sr - pr + nr);
           if (on) {  // max reductions are order-free; sums keep the per-lane row order
+            if (hl) cmu = fmax(cmu, clm);
+            if (hu) cmu = fmax(cmu, cum);
+            cmu = fmax(cmu, cpm);
+            pinfu = fmax(pinfu, pim);
             dinf = fmax(dinf, di);
             if (hl) cmr = fmax(cmr, cl);
             if (hu) cmr = fmax(cmr, cu);
@@ -1691,7 +1707,7 @@ __device__ __forceinline__ void resto_phase(const Params* __restrict__ prm, doub
             });
             return fmax(fmax(wmax(dn) / V[13], wmax(pinf)), wmax(cm) / V[14]);
           };
-          double se = sub_errR(V[4]);
+          double se = fmax(fmax(dinf / V[13], wmax(pinfu)), wmax(cmu) / V[14]);  // = sub_errR(V[4])
           bool done = false;
           while (se <= o.barrier_tol_factor * V[4] && !done) {
             double nmu = fmin(o.kappa_mu * V[4], pow(V[4], o.theta_mu));
