@@ -2223,6 +2223,8 @@ __device__ __forceinline__ int solve_one(Solver<CAP>& S, const Params* __restric
     STAMP0();
     // ===== optimality error (IpoptCalculatedQuantities::curr_nlp_error)
     double dinf = 0, cviol = 0, ucviol = 0, cmp = 0, sumy = 0, sumz = 0, sumv = 0, pinf = 0;
+    double cmu = 0;  // = compl_max(mu) of the barrier update below, from the same pass
+    const double muc = S.mu;
     bool bad = false;
     for (int i = S.lanef(); i < nw; i += WAVE) {
       const double g = S.grad_u(i) - S.zl[i] + S.zu[i];
@@ -2230,6 +2232,8 @@ __device__ __forceinline__ int solve_one(Solver<CAP>& S, const Params* __restric
       dinf = fmax(dinf, fabs(g));
       if (S.hasl(S.xl[i])) cmp = fmax(cmp, fabs((S.U[i] - S.xl[i]) * S.zl[i]));
       if (S.hasu(S.xu[i])) cmp = fmax(cmp, fabs((S.xu[i] - S.U[i]) * S.zu[i]));
+      if (S.hasl(S.xl[i])) cmu = fmax(cmu, fabs((S.U[i] - S.xl[i]) * S.zl[i] - muc));
+      if (S.hasu(S.xu[i])) cmu = fmax(cmu, fabs((S.xu[i] - S.U[i]) * S.zu[i] - muc));
       sumz += fabs(S.zl[i]) + fabs(S.zu[i]);
     }
     S.rows([&](int r, bool on) {
@@ -2245,6 +2249,9 @@ __device__ __forceinline__ int solve_one(Solver<CAP>& S, const Params* __restric
       if (hu) cv = fmax(cv, dr - hi);
       const double cu = fabs((hi - sr) * vur);
       if (hu) cmp = fmax(cmp, cu);
+      const double clm = fabs((sr - lo) * vlr - muc), cum = fabs((hi - sr) * vur - muc);
+      if (hl) cmu = fmax(cmu, clm);
+      if (hu) cmu = fmax(cmu, cum);
       const double ucv = cv / dcr;
       if (on) {
         cviol = fmax(cviol, cv);
@@ -2289,7 +2296,7 @@ __device__ __forceinline__ int solve_one(Solver<CAP>& S, const Params* __restric
     // ===== monotone barrier update (MonotoneMuUpdate::UpdateBarrierParameter)
     {
       const double base = fmax(dinf / sd, pinf);
-      double sub = fmax(base, S.compl_max(S.mu) / sc);
+      double sub = fmax(base, wmax(cmu) / sc);  // compl_max(S.mu)
       bool done = false, tsf = tiny_flag;
       while ((sub <= o.barrier_tol_factor * S.mu || tsf) && !done) {
         double nmu = fmin(o.kappa_mu * S.mu, pow(S.mu, o.theta_mu));
