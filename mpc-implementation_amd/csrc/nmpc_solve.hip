@@ -658,10 +658,8 @@ struct Solver {
   // barrier objective phi (oracle barrier_obj) at (u, s + a*ds) [sv == null -> s];
   // the sums are kept in rvars[32..33], so the accepted trial's sums serve the next
   // iteration's reference value (same slacks bit for bit: U <- Ut, s <- s + a ds)
-  __device__ __forceinline__ double barrier_obj(double f, const GLB double* u, const GLB double* sb, const GLB double* dsv,
-                                double a) {
-    STAMP0();
-    double logs = 0.0, damp = 0.0;
+  // per-lane partial sums: the control terms first, then the rows in rows() order
+  __device__ __forceinline__ void barrier_ctrl(const GLB double* u, double& logs, double& damp) const {
     for (int i = lanef(); i < nw; i += WAVE) {
       const bool lo = hasl(xl[i]), hi = hasu(xu[i]);
       if (lo) logs += log(u[i] - xl[i]);
@@ -669,22 +667,31 @@ struct Solver {
       if (lo && !hi) damp += u[i] - xl[i];
       if (hi && !lo) damp += xu[i] - u[i];
     }
-    rows([&](int r, bool on) {  // both logs of a row pair in flight; sums keep the per-lane row order
-      const double lo_ = dl[r], hi_ = du[r];
-      const double sv = dsv ? sb[r] + a * dsv[r] : sb[r];
-      const bool lo = hasl(lo_), hi = hasu(hi_);
-      const double ll = log(sv - lo_), lu = log(hi_ - sv);
-      if (on) {
-        if (lo) logs += ll;
-        if (hi) logs += lu;
-        if (lo && !hi) damp += sv - lo_;
-        if (hi && !lo) damp += hi_ - sv;
-      }
-    });
+  }
+  __device__ __forceinline__ void barrier_row(int r, bool on, double sv, double& logs, double& damp) const {
+    const double lo_ = dl[r], hi_ = du[r];
+    const bool lo = hasl(lo_), hi = hasu(hi_);
+    const double ll = log(sv - lo_), lu = log(hi_ - sv);  // both logs of a row pair in flight
+    if (on) {
+      if (lo) logs += ll;
+      if (hi) logs += lu;
+      if (lo && !hi) damp += sv - lo_;
+      if (hi && !lo) damp += hi_ - sv;
+    }
+  }
+  __device__ __forceinline__ double barrier_fin(double f, double logs, double damp) {
     logs = wsum(logs);
     damp = wsum(damp);
     rvars[32] = logs; rvars[33] = damp;
-    const double rr = phi_of(f, logs, damp);
+    return phi_of(f, logs, damp);
+  }
+  __device__ __forceinline__ double barrier_obj(double f, const GLB double* u, const GLB double* sb, const GLB double* dsv,
+                                double a) {
+    STAMP0();
+    double logs = 0.0, damp = 0.0;
+    barrier_ctrl(u, logs, damp);
+    rows([&](int r, bool on) { barrier_row(r, on, dsv ? sb[r] + a * dsv[r] : sb[r], logs, damp); });
+    const double rr = barrier_fin(f, logs, damp);
     STAMP1(PH_BARR);
     return rr;
   }
@@ -1271,19 +1278,33 @@ struct Solver {
     sync();
     rollout(Ut, Xt);
     fo = df * eval_fg(Xt, dt, dc);
-    double th = 0.0;
+    // theta_R, the barrier sums and the p/n sums in one pass over the rows (each
+    // accumulator keeps the per-lane order of barrier_obj / resto_pn_terms)
+    double th = 0.0, logs = 0.0, damp = 0.0, pn = 0.0, lg = 0.0, prox = 0.0;
     bool bad = false;
+    barrier_ctrl(Ut, logs, damp);
     rows([&](int r, bool on) {
       const double sv = s[r] + a * dss[r], pv = pR[r] + a * dps[r], nv = nR[r] + a * dns[r];
       const double dtr = dt[r];
+      barrier_row(r, on, sv, logs, damp);
+      const double l2 = log(pv) + log(nv);
       if (on) {
         th += fabs(dtr - sv - pv + nv);
         if (!isfinite(dtr)) bad = true;
+        pn += pv + nv;
+        lg += l2;
       }
     });
+    for (int i = lanef(); i < nw; i += WAVE) {
+      const double dd = Ut[i] - UR[i];
+      prox += dr2(i) * dd * dd;
+    }
     tht = wsum(th);
     if (wany(bad)) return false;
-    phit = barrier_obj(0.0, Ut, s, dss, a) + resto_pn_terms(Ut, a, dps, dns);
+    const double phb = barrier_fin(0.0, logs, damp);
+    pn = wsum(pn); lg = wsum(lg); prox = wsum(prox);
+    rvars[34] = pn; rvars[35] = lg; rvars[36] = prox;
+    phit = phb + pn_of(pn, lg, prox);
     return isfinite(phit);
   }
   __device__ __forceinline__ double frac_to_bound_resto(double tau_, const GLB double* dUs, const GLB double* dss,
@@ -1450,10 +1471,13 @@ struct Solver {
     sync();
     rollout(Ut, Xt);
     ft = df * eval_fg(Xt, dt, dc);
-    double th = 0.0;
+    // theta and the barrier sums in one pass over the rows
+    double th = 0.0, logs = 0.0, damp = 0.0;
     bool bad = false;
+    barrier_ctrl(Ut, logs, damp);
     rows([&](int r, bool on) {
       const double sv = s[r] + a * dss[r], dtr = dt[r];
+      barrier_row(r, on, sv, logs, damp);
       if (on) {
         th += fabs(dtr - sv);
         if (!isfinite(dtr)) bad = true;
@@ -1462,7 +1486,7 @@ struct Solver {
     tht = wsum(th);
     bad = wany(bad) || !isfinite(ft);
     if (bad) return false;
-    phit = barrier_obj(ft, Ut, s, dss, a);
+    phit = barrier_fin(ft, logs, damp);
     return isfinite(phit);
   }
 };
