@@ -1309,9 +1309,8 @@ struct Solver {
   }
   __device__ __forceinline__ double frac_to_bound_resto(double tau_, const GLB double* dUs, const GLB double* dss,
                                                         const GLB double* dps, const GLB double* dns) const {
-    double a = frac_to_bound(tau_, dUs, dss);
-    double b = 1.0;
-    rows([&](int r, bool on) {
+    double b = 1.0;  // p, n bounds in the same pass (min is order-free)
+    const double a = frac_to_bound_x(tau_, dUs, dss, [&](int r, bool on) {
       const double dp = dps[r], dn = dns[r], pr = pR[r], nr = nR[r];
       const double bp = (-tau_ * pr) / dp, bn = (-tau_ * nr) / dn;
       if (on && dp < 0) b = fmin(b, bp);
@@ -1321,9 +1320,8 @@ struct Solver {
   }
   __device__ __forceinline__ double dual_frac_to_bound_resto(double tau_, const GLB double* dUs, const GLB double* dss,
                                                              const GLB double* dps, const GLB double* dns) const {
-    double a = dual_frac_to_bound(tau_, dUs, dss);
     double b = 1.0;
-    rows([&](int r, bool on) {
+    const double a = dual_frac_to_bound_x(tau_, dUs, dss, [&](int r, bool on) {
       const double pr = pR[r], nr = nR[r], zp = zpR[r], zn = znR[r], dp = dps[r], dn = dns[r];
       const double dzp = mu / pr - zp - (zp / pr) * dp;
       const double dzn = mu / nr - zn - (zn / nr) * dn;
@@ -1336,6 +1334,12 @@ struct Solver {
 
   // primal fraction to the boundary (oracle frac_to_bound)
   __device__ __forceinline__ double frac_to_bound(double tau_, const GLB double* dUs, const GLB double* dss) const {
+    return frac_to_bound_x(tau_, dUs, dss, [](int, bool) {});
+  }
+  // ... with `extra(r, on)` run inside the same pass over the rows
+  template <class F>
+  __device__ __forceinline__ double frac_to_bound_x(double tau_, const GLB double* dUs, const GLB double* dss,
+                                                    F&& extra) const {
     STAMP0();
     double a = 1.0;
     for (int i = lanef(); i < nw; i += WAVE) {
@@ -1348,6 +1352,7 @@ struct Solver {
       const double al = (-tau_ * (sr - lo)) / dd, au = (-tau_ * (hi - sr)) / (-dd);
       if (on && hasl(lo) && dd < 0) a = fmin(a, al);
       if (on && hasu(hi) && -dd < 0) a = fmin(a, au);
+      extra(r, on);
     });
     a = wmin(a);
     STAMP1(PH_FTB);
@@ -1366,6 +1371,11 @@ struct Solver {
     if (hasu(du[r])) { const double iS = rcp(du[r] - s[r]); dvu = mu * iS - vu[r] + vu[r] * iS * dsv; }
   }
   __device__ __forceinline__ double dual_frac_to_bound(double tau_, const GLB double* dUs, const GLB double* dss) const {
+    return dual_frac_to_bound_x(tau_, dUs, dss, [](int, bool) {});
+  }
+  template <class F>
+  __device__ __forceinline__ double dual_frac_to_bound_x(double tau_, const GLB double* dUs, const GLB double* dss,
+                                                         F&& extra) const {
     STAMP0();
     double a = 1.0;
     for (int i = lanef(); i < nw; i += WAVE) {
@@ -1383,6 +1393,7 @@ struct Solver {
       const double b1 = (-tau_ * vlr) / a1, b2 = (-tau_ * vur) / a2;
       if (on && hl && a1 < 0) a = fmin(a, b1);
       if (on && hu && a2 < 0) a = fmin(a, b2);
+      extra(r, on);
     });
     a = wmin(a);
     STAMP1(PH_DFTB);
