@@ -3429,7 +3429,14 @@ int nmpc_closed_loop_dev(nmpc_handle* h, int32_t B, int32_t K, const double* lbx
     const int thr = 256;
     hipLaunchKernelGGL(nmpc_sched_init_kernel, dim3((unsigned)((n + thr - 1) / thr)), dim3(thr), 0,
                        (hipStream_t)stream, (int)B, (int)K, (const int*)order, q);
-    hipLaunchKernelGGL(h->sched, dim3(h->resident), dim3(WAVE), h->lds_bytes, (hipStream_t)stream,
+    // persistent waves: all resident ones (NMPC_SCHED_WAVES, a diagnostic, launches
+    // fewer: any count >= NXCD is correct since every launched wave is resident)
+    int waves = h->resident;
+    if (const char* ev = std::getenv("NMPC_SCHED_WAVES")) {
+      const int w = std::atoi(ev);
+      if (w >= NXCD && w < waves) waves = w;
+    }
+    hipLaunchKernelGGL(h->sched, dim3(waves), dim3(WAVE), h->lds_bytes, (hipStream_t)stream,
                        (const Params*)h->dprm, (int)B, io, lp, q);
     h->last_policy = 1;
     h->last_err = q.err;
