@@ -72,6 +72,9 @@ enum {
  * Python/NMPC_TT.py:257-265). */
 typedef struct nmpc_options {
   int32_t max_iter, acceptable_iter, max_soc, max_soft_resto_iters;
+  /* watchdog procedure of the backtracking line search (IPOPT defaults 10 and 3;
+   * a trigger of 0 disables it) */
+  int32_t watchdog_shortened_iter_trigger, watchdog_trial_iter_max;
   double tol, acceptable_tol, acceptable_obj_change_tol, acceptable_dual_inf_tol;
   double acceptable_constr_viol_tol, acceptable_compl_inf_tol;
   double dual_inf_tol, constr_viol_tol, compl_inf_tol;

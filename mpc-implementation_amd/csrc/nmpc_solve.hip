@@ -72,6 +72,9 @@ struct Lay {
   // restoration phase: reference/backup iterate, p/n and their multipliers, steps, filter
   int UR, zl0, zu0, s0, vl0, vu0, pR, nR, zpR, znR, dpR, dnR, dyR, dp2R, dn2R, dy2R, cms, filtR;
   int accU, accZl, accZu, accY;  // last acceptable iterate (BacktrackingLineSearch::StoreAcceptablePoint)
+  // watchdog procedure: the stored iterate and its step (main loop; the restoration phase
+  // reuses them, and adds its p, n, their multipliers and steps)
+  int wU, wzl, wzu, wdU, ws, wy, wvl, wvu, wds, wpR, wnR, wzpR, wznR, wdpR, wdnR, wdyR;
   // LDS
   int X, Xt, dX;
   int trig, qs, lam;
@@ -102,6 +105,10 @@ constexpr Lay make_layout(int N, int m) {
   L.dp2R = g; g += al8(ng); L.dn2R = g; g += al8(ng); L.dy2R = g; g += al8(ng); L.cms = g; g += al8(ng);
   L.filtR = g; g += al8(2 * FCAP + 2);
   L.accU = g; g += al8(nw); L.accZl = g; g += al8(nw); L.accZu = g; g += al8(nw); L.accY = g; g += al8(ng);
+  L.wU = g; g += al8(nw); L.wzl = g; g += al8(nw); L.wzu = g; g += al8(nw); L.wdU = g; g += al8(nw);
+  L.ws = g; g += al8(ng); L.wy = g; g += al8(ng); L.wvl = g; g += al8(ng); L.wvu = g; g += al8(ng);
+  L.wds = g; g += al8(ng); L.wpR = g; g += al8(ng); L.wnR = g; g += al8(ng); L.wzpR = g; g += al8(ng);
+  L.wznR = g; g += al8(ng); L.wdpR = g; g += al8(ng); L.wdnR = g; g += al8(ng); L.wdyR = g; g += al8(ng);
   L.wstotal = g;
   L.X = o; o += al2(nX); L.Xt = o; o += al2(nX); L.dX = o; o += al2(nX);
   L.trig = o; o += al2(8 * NS); L.qs = o; o += al2(10 * NS); L.lam = o; o += al2(8 * NS);
@@ -109,7 +116,7 @@ constexpr Lay make_layout(int N, int m) {
   L.P0 = o; o += 64; L.P1 = o; o += 64; L.pv0 = o; o += 8; L.pv1 = o; o += 8; L.St = o; o += 48;
   L.p = o; o += 64; L.ob = o; o += al2(2 * NMPC_MAX_OBS); L.inc = o; o += al2(8 * NS); L.red = o; o += 24;
   L.dl = o; o += al2(ng); L.du = o; o += al2(ng);  // row bounds (constant during a solve, read by every row pass)
-  L.rvars = o; o += 40;  // line-search / restoration scalars; [32..36] barrier sums
+  L.rvars = o; o += 48;  // line-search / restoration scalars; [32..36] barrier sums; [40..45] watchdog
   L.total = o;
   return L;
 }
@@ -298,6 +305,7 @@ struct Solver {
   GLB double* s, *y, *vl, *vu, *d, *dt, *ds, *ds2, *dc, *dms;
   GLB double *UR, *zl0, *zu0, *s0, *vl0, *vu0, *pR, *nR, *zpR, *znR, *dpR, *dnR, *dyR, *dp2R, *dn2R, *dy2R, *cms, *filtR;
   GLB double *accU, *accZl, *accZu, *accY;
+  GLB double *wU, *wzl, *wzu, *wdU, *wsl, *wy, *wvl, *wvu, *wds, *wpR, *wnR, *wzpR, *wznR, *wdpR, *wdnR, *wdyR;
   double rho, etaR;  // restoration: penalty, proximity weight * sqrt(mu)
   double* wsbase;    // workspace base of all scenarios (restoration re-binds from it)
   LDS double *dl, *du, *rvars;
@@ -331,6 +339,9 @@ struct Solver {
     dyR = gw + L.dyR; dp2R = gw + L.dp2R; dn2R = gw + L.dn2R; dy2R = gw + L.dy2R; cms = gw + L.cms;
     filtR = gw + L.filtR;
     accU = gw + L.accU; accZl = gw + L.accZl; accZu = gw + L.accZu; accY = gw + L.accY;
+    wU = gw + L.wU; wzl = gw + L.wzl; wzu = gw + L.wzu; wdU = gw + L.wdU; wsl = gw + L.ws; wy = gw + L.wy;
+    wvl = gw + L.wvl; wvu = gw + L.wvu; wds = gw + L.wds; wpR = gw + L.wpR; wnR = gw + L.wnR;
+    wzpR = gw + L.wzpR; wznR = gw + L.wznR; wdpR = gw + L.wdpR; wdnR = gw + L.wdnR; wdyR = gw + L.wdyR;
     gl = gw + L.gl; Hl = gw + L.Hl; trig = sm + L.trig; Qs = gw + L.Qs; qs = sm + L.qs;
     lam = sm + L.lam;
     K = gw + L.K; kf = sm + L.kf; Rk = gw + L.Rk; Kc = sm + L.Kc; Rc = sm + L.Rc;
@@ -1608,6 +1619,12 @@ __device__ __forceinline__ void resto_phase(const Params* __restrict__ prm, doub
       V[10] = -1e50; V[11] = -1e50;
       V[12] = io.f;            // original (scaled) objective at the restoration iterate
       int rstat = 1;        // 1 running, 0 back to the original problem, else final status
+      // the restoration phase's own watchdog procedure (its line search is a
+      // BacktrackingLineSearch with the same defaults); it reuses the main loop's watchdog
+      // storage, which is idle while restoration runs
+      int rwd_cnt = 0, rwd_trial = 0;
+      bool rin_wd = false;
+      volatile LDS double* WD = S.rvars + 40;
       auto lanef = [&]() { return S.lanef(); };  // for the STAMP macros
       (void)lanef;
       LDS double* stamps = S.stamps;
@@ -1826,21 +1843,74 @@ __device__ __forceinline__ void resto_phase(const Params* __restrict__ prm, doub
           }
           return ok && S.filter_ok(ph, th);
         };
+        // ---- watchdog (see the main loop): start, or judge against the stored reference
+        bool rwd_dir = false;  // the step is the stored one: its dual components use WD[4]
+        if (o.watchdog_shortened_iter_trigger > 0 && !rin_wd && rwd_cnt >= o.watchdog_shortened_iter_trigger) {
+          for (int i = S.lanef(); i < nw; i += WAVE) {
+            S.wU[i] = S.U[i]; S.wzl[i] = S.zl[i]; S.wzu[i] = S.zu[i]; S.wdU[i] = S.dU[i];
+          }
+          for (int r = S.lanef(); r < ng; r += WAVE) {
+            S.wsl[r] = S.s[r]; S.wy[r] = S.y[r]; S.wvl[r] = S.vl[r]; S.wvu[r] = S.vu[r]; S.wds[r] = S.ds[r];
+            S.wpR[r] = S.pR[r]; S.wnR[r] = S.nR[r]; S.wzpR[r] = S.zpR[r]; S.wznR[r] = S.znR[r];
+            S.wdpR[r] = S.dpR[r]; S.wdnR[r] = S.dnR[r]; S.wdyR[r] = S.dyR[r];
+          }
+          const double at = S.frac_to_bound_resto(V[5], S.dU, S.ds, S.dpR, S.dnR);
+          WD[0] = V[15]; WD[1] = V[16]; WD[2] = V[17]; WD[3] = at; WD[4] = V[4]; WD[5] = S.delta;
+          sync();
+          rin_wd = true;
+          rwd_trial = 0;
+        }
+        if (rin_wd) { V[15] = WD[0]; V[16] = WD[1]; V[17] = WD[2]; }
+        auto rwd_restore = [&]() {  // StopWatchDog
+          for (int i = S.lanef(); i < nw; i += WAVE) {
+            S.U[i] = S.wU[i]; S.zl[i] = S.wzl[i]; S.zu[i] = S.wzu[i]; S.dU[i] = S.wdU[i];
+          }
+          for (int r = S.lanef(); r < ng; r += WAVE) {
+            S.s[r] = S.wsl[r]; S.y[r] = S.wy[r]; S.vl[r] = S.wvl[r]; S.vu[r] = S.wvu[r]; S.ds[r] = S.wds[r];
+            S.pR[r] = S.wpR[r]; S.nR[r] = S.wnR[r]; S.zpR[r] = S.wzpR[r]; S.znR[r] = S.wznR[r];
+            S.dpR[r] = S.wdpR[r]; S.dnR[r] = S.wdnR[r]; S.dyR[r] = S.wdyR[r];
+          }
+          sync();
+          S.rollout(S.U, S.X);
+          V[12] = S.df * S.eval_fg(S.X, S.d, S.dc);
+          S.derivs(S.X, S.U);
+          V[15] = WD[0]; V[16] = WD[1]; V[17] = WD[2];
+          S.delta = WD[5];
+          rwd_dir = true;
+          rin_wd = false;
+          rwd_cnt = 0;
+        };
+        STAMPV0(_tls);
+        V[19] = 0.0; V[20] = 0.0; V[21] = 0.0;
+        int acc = 0, nsteps = 0;  // acc: 1 regular step, 2 SOC step
+        double a = 0.0, a_test = 0.0;
+        bool rskip = false, rforced = false;
+       while (true) {
+        V[18] = S.frac_to_bound_resto(V[5], S.dU, S.ds, S.dpR, S.dnR);
+        if (rin_wd) {
+          double fo_t, ph, th;
+          const bool ok_t = S.trial_resto(V[18], S.dU, S.ds, S.dpR, S.dnR, fo_t, ph, th);
+          const double at = WD[3];
+          if (ok_t && r_check(at, ph, th)) {
+            acc = 1; V[19] = V[18]; V[20] = fo_t; V[21] = ph; a_test = at; rin_wd = false;
+            break;
+          }
+          if (!ok_t || ++rwd_trial > o.watchdog_trial_iter_max) { rwd_restore(); rskip = true; continue; }
+          acc = 1; V[19] = V[18]; V[20] = fo_t; V[21] = ph; rforced = true;
+          break;
+        }
         double amin = o.gamma_theta;
         if (V[16] < 0) {
           amin = fmin(o.gamma_theta, o.gamma_phi * V[15] / (-V[16]));
           if (V[15] <= V[7]) amin = fmin(amin, o.delta * pow(V[15], o.s_theta) / pow(-V[16], o.s_phi));
         }
         amin *= o.alpha_min_frac;
-        STAMPV0(_tls);
-        V[18] = S.frac_to_bound_resto(V[5], S.dU, S.ds, S.dpR, S.dnR);
-        double a = V[18];
-        V[19] = 0.0; V[20] = 0.0; V[21] = 0.0;
-        int acc = 0, nsteps = 0;  // acc: 1 regular step, 2 SOC step
+        a = rskip ? V[18] * o.alpha_red_factor : V[18];
+        nsteps = 0;
         while (a > amin || nsteps == 0) {
           double fo_t, ph, th;
           const bool ok_t = S.trial_resto(a, S.dU, S.ds, S.dpR, S.dnR, fo_t, ph, th);
-          if (ok_t && r_check(a, ph, th)) { acc = 1; V[19] = a; V[20] = fo_t; V[21] = ph; break; }
+          if (ok_t && r_check(a, ph, th)) { acc = 1; V[19] = a; V[20] = fo_t; V[21] = ph; a_test = a; break; }
           if (ok_t && a == V[18] && V[15] <= th && o.max_soc > 0) {
             double th_tr = th, th_old = 0.0, a_soc = a;
             for (int r = S.lanef(); r < ng; r += WAVE) S.cms[r] = S.d[r] - S.s[r] - S.pR[r] + S.nR[r];
@@ -1864,7 +1934,10 @@ __device__ __forceinline__ void resto_phase(const Params* __restrict__ prm, doub
               dsp = S.ds2; dpp = S.dp2R; dnp = S.dn2R;
               double fo2, ph2, th2;
               if (!S.trial_resto(a_soc, S.dU2, S.ds2, S.dp2R, S.dn2R, fo2, ph2, th2)) break;
-              if (r_check(a, ph2, th2)) { acc = 2; V[19] = a_soc; V[20] = fo2; V[21] = ph2; soc_ok = true; break; }
+              if (r_check(a, ph2, th2)) {
+                acc = 2; V[19] = a_soc; V[20] = fo2; V[21] = ph2; a_test = a; soc_ok = true;
+                break;
+              }
               ++cnt;
               th_tr = th2;
             }
@@ -1873,8 +1946,11 @@ __device__ __forceinline__ void resto_phase(const Params* __restrict__ prm, doub
           a *= o.alpha_red_factor;
           ++nsteps;
         }
+        break;
+       }
         STAMPV1(_tls, PH_INIT);
         if (acc == 0) { rstat = ST_RESTO_FAIL; break; }  // no restoration inside the restoration phase
+        rwd_cnt = (nsteps == 0) ? 0 : rwd_cnt + 1;
         // filter augmentation (F-type + Armijo steps do not augment)
         {
           STAMP0();
@@ -1883,9 +1959,11 @@ __device__ __forceinline__ void resto_phase(const Params* __restrict__ prm, doub
           const GLB double* dpa = (acc == 2) ? S.dp2R : S.dpR;
           const GLB double* dna = (acc == 2) ? S.dn2R : S.dnR;
           const GLB double* dya = (acc == 2) ? S.dy2R : S.dyR;
-          if (!(r_ftype(a) && r_armijo(a, V[21])))
+          if (!rforced && !(r_ftype(a_test) && r_armijo(a_test, V[21])))
             S.filter_add(V[17] - o.gamma_phi * V[15], (1.0 - o.gamma_theta) * V[15]);
-          // ---- accept the restoration trial point
+          // ---- accept the restoration trial point (the step's dual components with its
+          //      own mu, the kappa_sigma safeguard with the current one)
+          if (rwd_dir) S.mu = WD[4];
           const double ad = S.dual_frac_to_bound_resto(V[5], dUa, dsa, dpa, dna);
           for (int i = S.lanef(); i < nw; i += WAVE) {
             double dzl, dzu;
@@ -1899,6 +1977,7 @@ __device__ __forceinline__ void resto_phase(const Params* __restrict__ prm, doub
             S.zl[i] = nzl; S.zu[i] = nzu;
           }
           const double muR = V[4], aP = V[19];  // volatile LDS scalars read once
+          const double dmuR = rwd_dir ? (double)WD[4] : muR;
           S.rows([&](int r, bool on) {
             const double sr = S.s[r], lo = S.dl[r], hi = S.du[r], vlr = S.vl[r], vur = S.vu[r];
             const double dsr = dsa[r], dpr = dpa[r], dnr = dna[r], dyr = dya[r];
@@ -1907,8 +1986,8 @@ __device__ __forceinline__ void resto_phase(const Params* __restrict__ prm, doub
             double dvl = 0.0, dvu = 0.0;  // dv_s with the loads hoisted
             if (hl) { const double iS = rcp(sr - lo); dvl = S.mu * iS - vlr - vlr * iS * dsr; }
             if (hu) { const double iS = rcp(hi - sr); dvu = S.mu * iS - vur + vur * iS * dsr; }
-            const double dzp = muR / pr - zp - (zp / pr) * dpr;
-            const double dzn = muR / nr - zn - (zn / nr) * dnr;
+            const double dzp = dmuR / pr - zp - (zp / pr) * dpr;
+            const double dzn = dmuR / nr - zn - (zn / nr) * dnr;
             const double sn = sr + aP * dsr;
             const double pn = pr + aP * dpr, nn = nr + aP * dnr;
             double nvl = vlr + ad * dvl, nvu = vur + ad * dvu;
@@ -1927,6 +2006,7 @@ __device__ __forceinline__ void resto_phase(const Params* __restrict__ prm, doub
               S.d[r] = dtr;
             }
           });
+          S.mu = V[4];
           for (int i = S.lanef(); i < nw; i += WAVE) S.U[i] = S.Ut[i];
           if (S.lanef() <= N) {
 #pragma unroll
@@ -2250,6 +2330,12 @@ __device__ __forceinline__ int solve_one(Solver<CAP>& S, const Params* __restric
   bool running = (status == 0);
   bool need_resto = false;
   RestoIO rio;
+  // watchdog procedure (BacktrackingLineSearch): successive shortened steps, active
+  // flag, trial iterations; WD = reference values of the stored point and its step
+  // [0] theta, [1] phi, [2] grad(phi)^T d, [3] alpha test, [4] mu, [5] delta of the step
+  int wd_cnt = 0, wd_trial = 0;
+  bool in_wd = false;
+  volatile LDS double* WD = S.rvars + 40;
 
   while (running) {
   while (true) {
@@ -2411,7 +2497,7 @@ __device__ __forceinline__ int solve_one(Solver<CAP>& S, const Params* __restric
       STAMP1(PH_LSSET);
     }
     STAMPV0(_tls);  // whole line search incl. nested phases (diagnostic slot of the old Riccati step 3)
-    const double phi_ref = phic ? S.phi_of(f, S.rvars[32], S.rvars[33]) : S.barrier_obj(f, S.U, S.s, nullptr, 0.0);
+    double phi_ref = phic ? S.phi_of(f, S.rvars[32], S.rvars[33]) : S.barrier_obj(f, S.U, S.s, nullptr, 0.0);
     if (MV[0] < 0) {
       MV[0] = o.theta_max_fact * fmax(1.0, theta_ref);
       MV[1] = o.theta_min_fact * fmax(1.0, theta_ref);
@@ -2445,12 +2531,65 @@ __device__ __forceinline__ int solve_one(Solver<CAP>& S, const Params* __restric
     double alpha_p = 0.0, alpha_d = 0.0, f_acc = 0.0;
     int ls_trials = 0;
     double a_test_acc = 0.0, phi_acc = 0.0;
+    int n_acc = 0;          // backtracking steps before the accepted trial
+    bool wd_forced = false; // a watchdog trial iteration: full step taken unchecked
+
+    // ===== watchdog procedure (BacktrackingLineSearch::FindAcceptableTrialPoint)
+    // tiny step detection (BacktrackingLineSearch::DetectTinyStep; ratios from row_step_ls)
+    bool tiny = tiny_mx <= o.tiny_step_tol && tiny_msv <= o.tiny_step_tol && pinf <= 1e-4;
+    // the dual step of the step being taken is formed with the mu / delta it was computed
+    // with: after StopWatchDog that is the stored step's (WD[4], WD[5])
+    bool wd_dir = false;
+    auto dir_mu = [&]() { return wd_dir ? (double)WD[4] : mu; };
+    // StopWatchDog: back to the stored iterate, its step and its reference values
+    auto wd_restore = [&]() {
+      for (int i = S.lanef(); i < nw; i += WAVE) {
+        S.U[i] = S.wU[i]; S.zl[i] = S.wzl[i]; S.zu[i] = S.wzu[i]; S.dU[i] = S.wdU[i];
+      }
+      for (int r = S.lanef(); r < ng; r += WAVE) {
+        S.s[r] = S.wsl[r]; S.y[r] = S.wy[r]; S.vl[r] = S.wvl[r]; S.vu[r] = S.wvu[r]; S.ds[r] = S.wds[r];
+      }
+      sync();
+      S.rollout(S.U, S.X);
+      f = S.df * S.eval_fg(S.X, S.d, S.dc);
+      S.derivs(S.X, S.U);
+      S.adjoint(S.df, S.y);  // grad of the Lagrangian there (soft restoration's pd error)
+      theta_ref = WD[0]; phi_ref = WD[1]; gbd = WD[2];
+      S.delta = WD[5];
+      wd_dir = true;
+      phic = false;
+      in_wd = false;
+      wd_cnt = 0;
+    };
+    if (in_wd && tiny) {  // a tiny step inside the watchdog stops it
+      wd_restore();
+      tiny = false;
+    }
+    if (o.watchdog_shortened_iter_trigger > 0 && !in_wd && !tiny && !in_soft &&
+        wd_cnt >= o.watchdog_shortened_iter_trigger) {  // StartWatchDog
+      for (int i = S.lanef(); i < nw; i += WAVE) {
+        S.wU[i] = S.U[i]; S.wzl[i] = S.zl[i]; S.wzu[i] = S.zu[i]; S.wdU[i] = S.dU[i];
+      }
+      for (int r = S.lanef(); r < ng; r += WAVE) {
+        S.wsl[r] = S.s[r]; S.wy[r] = S.y[r]; S.wvl[r] = S.vl[r]; S.wvu[r] = S.vu[r]; S.wds[r] = S.ds[r];
+      }
+      const double at = S.frac_to_bound(tau, S.dU, S.ds);
+      WD[0] = theta_ref; WD[1] = phi_ref; WD[2] = gbd; WD[3] = at; WD[4] = mu; WD[5] = S.delta;
+      sync();
+      in_wd = true;
+      wd_trial = 0;
+    }
+    if (in_wd) {  // FilterLSAcceptor::InitThisLineSearch(in_watchdog): the stored reference
+      theta_ref = WD[0]; phi_ref = WD[1]; gbd = WD[2];
+    }
 
     // soft restoration step (BacktrackingLineSearch::TrySoftRestoStep); returns
     // 0 rejected, 1 accepted, 2 accepted & satisfies the original criterion
     auto try_soft = [&]() -> int {
       const double ap = S.frac_to_bound(tau, S.dU, S.ds);
+      S.mu = dir_mu();  // dual components of the step (its own mu); the barrier terms use mu
       const double ad = S.dual_frac_to_bound(tau, S.dU, S.ds);
+      S.mu = mu;
       const double a = fmin(ap, ad);
       // current pd error (grad_lag from the adjoint computed at loop start)
       double dual = 0, prim = 0, cm = 0;
@@ -2473,6 +2612,7 @@ __device__ __forceinline__ int solve_one(Solver<CAP>& S, const Params* __restric
       // trial multipliers into the "2" buffers: dU2 <- (unused) ; stage them in place later
       // evaluate grad_lag at the trial point: derivatives + adjoint with trial y
       // (overwrites the current derivative data; if rejected the solve stops)
+      S.mu = dir_mu();
       for (int r = S.lanef(); r < ng; r += WAVE) {
         double D, rs;
         S.row_rs(r, D, rs);
@@ -2503,6 +2643,7 @@ __device__ __forceinline__ int solve_one(Solver<CAP>& S, const Params* __restric
         if (S.hasl(S.dl[r])) cm2 += fabs((sv - S.dl[r]) * vlt - mu);
         if (S.hasu(S.du[r])) cm2 += fabs((S.du[r] - sv) * vut - mu);
       }
+      S.mu = mu;
       const double e_t = wsum(dual2) / nn + (ng ? wsum(prim2) / ng : 0.0) + (nc ? wsum(cm2) / nc : 0.0);
       if (e_t <= o.soft_resto_pderror_reduction_factor * e_c) {
         alpha_p = a; alpha_d = a; f_acc = ft;
@@ -2521,8 +2662,6 @@ __device__ __forceinline__ int solve_one(Solver<CAP>& S, const Params* __restric
         if (r == 2) in_soft = false;
       }
     } else {
-      // tiny step detection (BacktrackingLineSearch::DetectTinyStep; ratios from row_step_ls)
-      const bool tiny = tiny_mx <= o.tiny_step_tol && tiny_msv <= o.tiny_step_tol && pinf <= 1e-4;
       if (tiny) {
         const double a = S.frac_to_bound(tau, S.dU, S.ds);
         double ft, phit, tht;
@@ -2532,6 +2671,30 @@ __device__ __forceinline__ int solve_one(Solver<CAP>& S, const Params* __restric
           tiny_flag = true;
         }
       } else {
+       bool skip_first = false;  // after StopWatchDog: the stored step's full step was rejected
+       while (true) {
+        if (in_wd) {
+          // one trial at the full step, judged against the stored reference values with
+          // the stored alpha test, no SOC (BacktrackingLineSearch::DoBacktrackingLineSearch)
+          const double amax_w = S.frac_to_bound(tau, S.dU, S.ds);
+          double ft, phit, tht;
+          ++ls_trials;
+          const bool okev = S.trial(amax_w, S.dU, S.ds, ft, phit, tht);
+          const double at = WD[3];
+          if (okev && check_accept(at, phit, tht)) {  // watchdog procedure successful
+            acc_kind = 1; alpha_p = amax_w; f_acc = ft; a_test_acc = at; phi_acc = phit;
+            in_wd = false;
+            break;
+          }
+          if (!okev || ++wd_trial > o.watchdog_trial_iter_max) {
+            wd_restore();
+            skip_first = true;
+            continue;
+          }
+          acc_kind = 1; alpha_p = amax_w; f_acc = ft;  // watchdog trial iteration
+          wd_forced = true;
+          break;
+        }
         double amin = o.gamma_theta;
         if (gbd < 0) {
           amin = fmin(o.gamma_theta, o.gamma_phi * theta_ref / (-gbd));
@@ -2540,14 +2703,14 @@ __device__ __forceinline__ int solve_one(Solver<CAP>& S, const Params* __restric
         }
         amin *= o.alpha_min_frac;
         const double amax_p = S.frac_to_bound(tau, S.dU, S.ds);
-        double a = amax_p;
+        double a = skip_first ? amax_p * o.alpha_red_factor : amax_p;
         int n_steps = 0;
         while (a > amin || n_steps == 0) {
           double ft, phit, tht;
           ++ls_trials;
           const bool okev = S.trial(a, S.dU, S.ds, ft, phit, tht);
           if (okev && check_accept(a, phit, tht)) {
-            acc_kind = 1; alpha_p = a; f_acc = ft; a_test_acc = a; phi_acc = phit;
+            acc_kind = 1; alpha_p = a; f_acc = ft; a_test_acc = a; phi_acc = phit; n_acc = n_steps;
             break;
           }
           if (okev && a == amax_p && theta_ref <= tht && o.max_soc > 0) {
@@ -2574,7 +2737,7 @@ __device__ __forceinline__ int solve_one(Solver<CAP>& S, const Params* __restric
               ++ls_trials;
               if (!S.trial(a_soc, S.dU2, S.ds2, ft2, phit2, tht2)) break;
               if (check_accept(a, phit2, tht2)) {
-                acc_kind = 2; alpha_p = a_soc; f_acc = ft2; a_test_acc = a; phi_acc = phit2;
+                acc_kind = 2; alpha_p = a_soc; f_acc = ft2; a_test_acc = a; phi_acc = phit2; n_acc = n_steps;
                 soc_acc = true;
                 break;
               }
@@ -2586,16 +2749,20 @@ __device__ __forceinline__ int solve_one(Solver<CAP>& S, const Params* __restric
           a *= o.alpha_red_factor;
           ++n_steps;
         }
+        break;
+       }
         if (acc_kind == 0) {
           const int r = try_soft();
           if (r > 0) derivs_done = true;
           if (r == 1) { in_soft = true; soft_cnt = 0; }
-        } else {
+        } else if (!wd_forced) {
           if (!(is_ftype(a_test_acc) && armijo(a_test_acc, phi_acc)))
             S.filter_add(phi_ref - o.gamma_phi * theta_ref, (1.0 - o.gamma_theta) * theta_ref);
         }
       }
     }
+    // successive shortened steps (regular, tiny and watchdog steps) trigger the watchdog
+    if (acc_kind == 1 || acc_kind == 2) wd_cnt = (n_acc == 0) ? 0 : wd_cnt + 1;
     if (acc_kind == 0) {
       // ===== feasibility restoration phase (BacktrackingLineSearch -> RestoMinC_1Nrm;
       //       oracle restoration())
@@ -2624,6 +2791,7 @@ __device__ __forceinline__ int solve_one(Solver<CAP>& S, const Params* __restric
       STAMP0();
       const GLB double* dUa = (acc_kind == 2) ? S.dU2 : S.dU;
       const GLB double* dsa = (acc_kind == 2) ? S.ds2 : S.ds;
+      S.mu = dir_mu();  // the step's dual components (mu below: the kappa_sigma safeguard)
       if (acc_kind != 3) alpha_d = S.dual_frac_to_bound(tau, dUa, dsa);
       const double ap = alpha_p, ad = alpha_d;
       const double ks = o.kappa_sigma;
@@ -2664,6 +2832,7 @@ __device__ __forceinline__ int solve_one(Solver<CAP>& S, const Params* __restric
           S.d[r] = dtr;
         }
       });
+      S.mu = mu;
       for (int i = S.lanef(); i < nw; i += WAVE) S.U[i] = S.Ut[i];
       if (S.lanef() <= N) {
 #pragma unroll
@@ -2700,6 +2869,7 @@ __device__ __forceinline__ int solve_one(Solver<CAP>& S, const Params* __restric
   f = rio.f;
   in_soft = false;
   phic = false;
+  wd_cnt = 0;
   }
 
   // ---------------- outputs (honor_original_bounds)
@@ -3097,6 +3267,7 @@ extern "C" {
 void nmpc_default_options(nmpc_options* o) {
   std::memset(o, 0, sizeof(*o));
   o->max_iter = 3000; o->acceptable_iter = 15; o->max_soc = 4; o->max_soft_resto_iters = 10;
+  o->watchdog_shortened_iter_trigger = 10; o->watchdog_trial_iter_max = 3;
   o->tol = 1e-8; o->acceptable_tol = 1e-6; o->acceptable_obj_change_tol = 1e20;
   o->acceptable_dual_inf_tol = 1e10; o->acceptable_constr_viol_tol = 1e-2; o->acceptable_compl_inf_tol = 1e-2;
   o->dual_inf_tol = 1.0; o->constr_viol_tol = 1e-4; o->compl_inf_tol = 1e-4;

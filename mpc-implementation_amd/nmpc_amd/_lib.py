@@ -26,7 +26,8 @@ EXPORTS = (
     "nmpc_shift_dev", "nmpc_closed_loop_dev", "nmpc_closed_loop_info", "nmpc_last_error", "nmpc_kernel_info",
 )
 
-_OPT_INT = ("max_iter", "acceptable_iter", "max_soc", "max_soft_resto_iters")
+_OPT_INT = ("max_iter", "acceptable_iter", "max_soc", "max_soft_resto_iters",
+            "watchdog_shortened_iter_trigger", "watchdog_trial_iter_max")
 _OPT_DBL = (
     "tol", "acceptable_tol", "acceptable_obj_change_tol", "acceptable_dual_inf_tol",
     "acceptable_constr_viol_tol", "acceptable_compl_inf_tol",

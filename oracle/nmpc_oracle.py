@@ -45,8 +45,9 @@ restoration phase (min rho*sum(p+n) + eta/2*|D_R(x-x_R)|^2 s.t. d(x)-p+n in
 [d_L,d_U], its own filter line search, return test against the original
 filter, bound-multiplier reconstruction), return to the last acceptable point
 when restoration is called at an almost feasible point, optimal/acceptable/
-max-iter/infeasible termination, honor_original_bounds.  NOT restated: the
-watchdog procedure.
+max-iter/infeasible termination, honor_original_bounds, and the watchdog
+procedure (watchdog_shortened_iter_trigger / watchdog_trial_iter_max) in the
+main and the restoration line search.
 """
 from __future__ import annotations
 
@@ -525,6 +526,8 @@ IPOPT_DEFAULTS = dict(
     perturb_inc_fact=8.0, perturb_dec_fact=1.0 / 3.0,
     tiny_step_tol=10 * EPS, soft_resto_pderror_reduction_factor=0.9999,
     max_soft_resto_iters=10,
+    # watchdog procedure (BacktrackingLineSearch::StartWatchDog / StopWatchDog)
+    watchdog_shortened_iter_trigger=10, watchdog_trial_iter_max=3,
     # feasibility restoration phase (RestoMinC_1Nrm / RestoIpoptNLP defaults)
     resto_penalty_parameter=1000.0, resto_proximity_weight=1.0,
     required_infeasibility_reduction=0.9, bound_mult_reset_threshold=1000.0,
@@ -573,6 +576,8 @@ class IpoptDense:
         """IPOPT DefaultIterateInitializer::push_variables."""
         x = x.copy()
         both = lm & um
+        lo = np.where(lm, lo, 0.0)  # absent bounds never enter the arithmetic (no inf - inf)
+        hi = np.where(um, hi, 0.0)
         pl = kp * np.maximum(1.0, np.abs(lo))
         pu = kp * np.maximum(1.0, np.abs(hi))
         span = np.where(both, hi - lo, np.inf)
@@ -655,8 +660,11 @@ class IpoptDense:
         def barrier_obj(f_, x_, s_, mu_):
             Sxl, Sxu, Ssl, Ssu = slacks(x_, s_)
             val = f_
-            val -= mu_ * (np.sum(np.log(Sxl[xlm])) + np.sum(np.log(Sxu[xum]))
-                          + np.sum(np.log(Ssl[slm])) + np.sum(np.log(Ssu[sum_])))
+            # a trial slack that rounds to exactly 0 gives log 0 = -inf: phi is then not
+            # finite and the trial counts as an evaluation error (as on the device)
+            with np.errstate(divide="ignore"):
+                val -= mu_ * (np.sum(np.log(Sxl[xlm])) + np.sum(np.log(Sxu[xum]))
+                              + np.sum(np.log(Ssl[slm])) + np.sum(np.log(Ssu[sum_])))
             val += o["kappa_d"] * mu_ * (np.dot(damp_xl, Sxl * xlm) + np.dot(damp_xu, Sxu * xum)
                                          + np.dot(damp_sl, Ssl * slm) + np.dot(damp_su, Ssu * sum_))
             return val
@@ -718,6 +726,11 @@ class IpoptDense:
         tr = []
         status = None
         acc_point = None
+        # watchdog procedure (BacktrackingLineSearch): successive shortened steps,
+        # active flag, trial iterations, the stored point / step / reference values
+        wd_cnt, in_wd, wd_trial, wd_point, wd_alpha = 0, False, 0, None, 1.0
+        self.wd_events = {"start": 0, "stop": 0, "success": 0, "resto_start": 0, "resto_stop": 0}
+        wd_trigger, wd_max = o["watchdog_shortened_iter_trigger"], o["watchdog_trial_iter_max"]
 
         def nlp_error(x_, s_, d_, gf_, J_, y_, zl_, zu_, vl_, vu_):
             sd, sc = err_scaling(y_, zl_, zu_, vl_, vu_)
@@ -794,9 +807,10 @@ class IpoptDense:
             def phiR(x_, s_, p_, n_, mu_):
                 Sxl, Sxu, Ssl, Ssu = slacks(x_, s_)
                 val = fR(x_, p_, n_, mu_)
-                val -= mu_ * (np.sum(np.log(Sxl[xlm])) + np.sum(np.log(Sxu[xum]))
-                              + np.sum(np.log(Ssl[slm])) + np.sum(np.log(Ssu[sum_]))
-                              + np.sum(np.log(p_)) + np.sum(np.log(n_)))
+                with np.errstate(divide="ignore"):  # log 0 = -inf -> evaluation error (barrier_obj)
+                    val -= mu_ * (np.sum(np.log(Sxl[xlm])) + np.sum(np.log(Sxu[xum]))
+                                  + np.sum(np.log(Ssl[slm])) + np.sum(np.log(Ssu[sum_]))
+                                  + np.sum(np.log(p_)) + np.sum(np.log(n_)))
                 val += o["kappa_d"] * mu_ * (np.dot(damp_xl, Sxl * xlm) + np.dot(damp_xu, Sxu * xum)
                                              + np.dot(damp_sl, Ssl * slm) + np.dot(damp_su, Ssu * sum_)
                                              + np.sum(p_) + np.sum(n_))
@@ -846,6 +860,7 @@ class IpoptDense:
             dlast, dcurr = 0.0, 0.0
             first = True
             racc, rlast_obj, rcurr_obj, rlast_it = 0, -1e50, -1e50, -1
+            rwd_cnt, rin_wd, rwd_trial, rwd_point, rwd_alpha = 0, False, 0, None, 1.0
             xx, ss = xR_, sR
             while True:
                 # ---- progress w.r.t. the original problem (RestoConvergenceCheck)
@@ -1024,44 +1039,77 @@ class IpoptDense:
                         return None
                     return xt, s_t, pt, nt, evt, dtt, ph, thetaR(dtt, s_t, pt, nt)
 
-                amin = o["gamma_theta"]
-                if gbd < 0:
-                    amin = min(o["gamma_theta"], o["gamma_phi"] * th_ref / (-gbd))
-                    if th_ref <= th_min:
-                        amin = min(amin, o["delta"] * th_ref ** o["s_theta"] / (-gbd) ** o["s_phi"])
-                amin *= o["alpha_min_frac"]
-                amax_p = ftb_R(tauR, xx, ss, pp, nn, stp[0], stp[1], stp[3], stp[10])
-                a = amax_p
-                nsteps = 0
-                acc = None
-                while a > amin or nsteps == 0:
-                    tri = r_trial(a, stp)
-                    if tri is not None and r_check(a, tri[6], tri[7]):
-                        acc = (a, stp, tri)
+                def r_line_search(skip_first):
+                    """DoBacktrackingLineSearch of the restoration NLP on `stp` (see the main
+                    loop's line_search): (accepted, n_steps, a_test, eval_error, first trial)."""
+                    amax_p = ftb_R(tauR, xx, ss, pp, nn, stp[0], stp[1], stp[3], stp[10])
+                    if rin_wd:
+                        tri = r_trial(amax_p, stp)
+                        if tri is not None and r_check(rwd_alpha, tri[6], tri[7]):
+                            return (amax_p, stp, tri), 0, rwd_alpha, False, tri
+                        return None, 0, rwd_alpha, tri is None, tri
+                    amin = o["gamma_theta"]
+                    if gbd < 0:
+                        amin = min(o["gamma_theta"], o["gamma_phi"] * th_ref / (-gbd))
+                        if th_ref <= th_min:
+                            amin = min(amin, o["delta"] * th_ref ** o["s_theta"] / (-gbd) ** o["s_phi"])
+                    amin *= o["alpha_min_frac"]
+                    a = amax_p * (o["alpha_red_factor"] if skip_first else 1.0)
+                    n_ = 0
+                    while a > amin or n_ == 0:
+                        tri = r_trial(a, stp)
+                        if tri is not None and r_check(a, tri[6], tri[7]):
+                            return (a, stp, tri), n_, a, False, None
+                        if tri is not None and a == amax_p and th_ref <= tri[7] and o["max_soc"] > 0:
+                            th_tr, th_old, a_soc, cms, cnt, cur = tri[7], 0.0, a, cR.copy(), 0, tri
+                            while cnt < o["max_soc"] and (cnt == 0 or th_tr <= o["kappa_soc"] * th_old):
+                                th_old = th_tr
+                                cms = a_soc * cms + (cur[5] - cur[1] - cur[2] + cur[3])
+                                st2 = rdir(cms)
+                                a_soc = ftb_R(tauR, xx, ss, pp, nn, st2[0], st2[1], st2[3], st2[10])
+                                cur = r_trial(a_soc, st2)
+                                if cur is None:
+                                    break
+                                if r_check(a, cur[6], cur[7]):
+                                    return (a_soc, st2, cur), n_, a, False, None
+                                cnt += 1
+                                th_tr = cur[7]
+                        a *= o["alpha_red_factor"]
+                        n_ += 1
+                    return None, n_, a, False, None
+
+                # ---- watchdog procedure of the restoration phase's own line search
+                if wd_trigger > 0 and not rin_wd and rwd_cnt >= wd_trigger:
+                    rwd_point = (xx, ss, pp, nn, evR, dR, JR, yR, zlR, zuR, vlR, vuR, zp, zn, stp,
+                                 th_ref, ph_ref, gbd)
+                    rwd_alpha = ftb_R(tauR, xx, ss, pp, nn, stp[0], stp[1], stp[3], stp[10])
+                    rwd_trial, rin_wd = 0, True
+                    self.wd_events["resto_start"] += 1
+                if rin_wd:
+                    th_ref, ph_ref, gbd = rwd_point[15], rwd_point[16], rwd_point[17]
+                skip_first, forced = False, False
+                while True:
+                    acc, nsteps, a, ev_err, wtri = r_line_search(skip_first)
+                    if not rin_wd:
                         break
-                    if tri is not None and a == amax_p and th_ref <= tri[7] and o["max_soc"] > 0:
-                        th_tr, th_old, a_soc, cms, cnt, cur = tri[7], 0.0, a, cR.copy(), 0, tri
-                        while cnt < o["max_soc"] and (cnt == 0 or th_tr <= o["kappa_soc"] * th_old):
-                            th_old = th_tr
-                            cms = a_soc * cms + (cur[5] - cur[1] - cur[2] + cur[3])
-                            st2 = rdir(cms)
-                            a_soc = ftb_R(tauR, xx, ss, pp, nn, st2[0], st2[1], st2[3], st2[10])
-                            cur = r_trial(a_soc, st2)
-                            if cur is None:
-                                break
-                            if r_check(a, cur[6], cur[7]):
-                                acc = (a_soc, st2, cur)
-                                break
-                            cnt += 1
-                            th_tr = cur[7]
-                        if acc is not None:
-                            break
-                    a *= o["alpha_red_factor"]
-                    nsteps += 1
+                    if acc is not None:
+                        rin_wd = False
+                        break
+                    rwd_trial += 1
+                    if ev_err or rwd_trial > wd_max:
+                        (xx, ss, pp, nn, evR, dR, JR, yR, zlR, zuR, vlR, vuR, zp, zn, stp,
+                         th_ref, ph_ref, gbd) = rwd_point
+                        rin_wd, rwd_cnt, skip_first = False, 0, True
+                        self.wd_events["resto_stop"] += 1
+                        continue
+                    acc = (ftb_R(tauR, xx, ss, pp, nn, stp[0], stp[1], stp[3], stp[10]), stp, wtri)
+                    forced = True
+                    break
                 if acc is None:  # no restoration inside the restoration phase
                     return dict(status=RESTORATION_FAILED, it=it_, x=xx)
+                rwd_cnt = 0 if nsteps == 0 else rwd_cnt + 1
                 a_acc, st, tri = acc
-                if not (r_ftype(a) and r_armijo(a, tri[6])):
+                if not forced and not (r_ftype(a) and r_armijo(a, tri[6])):
                     rfilt.append((ph_ref - o["gamma_phi"] * th_ref, (1.0 - o["gamma_theta"]) * th_ref))
                 ad = dftb_R(tauR, zlR, zuR, vlR, vuR, zp, zn, st)
                 xx, ss, pp, nn, evR, dR = tri[0], tri[1], tri[2], tri[3], tri[4], tri[5]
@@ -1295,16 +1343,83 @@ class IpoptDense:
                     return (a, a, xt, st, evt, ft, dt, yt, zlt, zut, vlt, vut, orig)
                 return None
 
+            def line_search(skip_first):
+                """BacktrackingLineSearch::DoBacktrackingLineSearch on `step` from the
+                current point.  Returns (accepted, n_steps, trials, soc, a_test, eval_error,
+                first trial).  In the watchdog procedure only the full step is tried, with
+                the watchdog's reference values and alpha test, and no SOC."""
+                dx_, ds_ = step[0], step[1]
+                amax_p = frac_to_bound(tau, x, s, dx_, ds_)
+                if in_wd:
+                    tri = trial(amax_p, dx_, ds_)
+                    if tri is not None and check_accept(wd_alpha, tri[5], tri[6]):
+                        return ("reg", amax_p, step, tri), 0, 1, False, wd_alpha, False, tri
+                    return None, 0, 1, False, wd_alpha, tri is None, tri
+                amin = o["gamma_theta"]
+                if gBD < 0:
+                    amin = min(o["gamma_theta"], o["gamma_phi"] * theta_ref / (-gBD))
+                    if theta_ref <= theta_min:
+                        amin = min(amin, o["delta"] * theta_ref ** o["s_theta"] / (-gBD) ** o["s_phi"])
+                amin *= o["alpha_min_frac"]
+                a = amax_p * (o["alpha_red_factor"] if skip_first else 1.0)
+                n_ = 0
+                trials = 0
+                while a > amin or n_ == 0:
+                    trials += 1
+                    tri = trial(a, dx_, ds_)
+                    if tri is not None and check_accept(a, tri[5], tri[6]):
+                        return ("reg", a, step, tri), n_, trials, False, a, False, None
+                    if tri is not None and a == amax_p and theta_ref <= tri[6] and o["max_soc"] > 0:
+                        # second-order correction (FilterLSAcceptor::TrySecondOrderCorrection)
+                        th_tr = tri[6]
+                        th_old = 0.0
+                        a_soc = a
+                        dms = rd.copy()
+                        cnt = 0
+                        cur = tri
+                        while cnt < o["max_soc"] and (cnt == 0 or th_tr <= o["kappa_soc"] * th_old):
+                            th_old = th_tr
+                            dms = a_soc * dms + (cur[4] - cur[1])
+                            stp = solve_dir(dms)
+                            a_soc = frac_to_bound(tau, x, s, stp[0], stp[1])
+                            cur = trial(a_soc, stp[0], stp[1])
+                            trials += 1
+                            if cur is None:
+                                break
+                            if check_accept(a, cur[5], cur[6]):
+                                return ("reg", a_soc, stp, cur), n_, trials, True, a, False, None
+                            cnt += 1
+                            th_tr = cur[6]
+                    a *= o["alpha_red_factor"]
+                    n_ += 1
+                return None, n_, trials, False, a, False, None
+
             accepted = None
             ls_trials = 0
             soc_taken = False
             alpha_p = 0.0
             alpha_d = 0.0
+            n_steps = 0
             # tiny step detection
             tiny = (amax(dx / (1.0 + np.abs(x))) <= o["tiny_step_tol"]
                     and amax(ds / (1.0 + np.abs(s))) <= o["tiny_step_tol"]
                     and amax(rd) <= 1e-4)
             step = (dx, ds, dy, dzl, dzu, dvl, dvu)
+            # ---- watchdog procedure (BacktrackingLineSearch::FindAcceptableTrialPoint)
+            if in_wd and tiny:
+                # tiny step inside the watchdog: back to its stored point (StopWatchDog)
+                x, s, y, zl, zu, vl, vu, ev, step, theta_ref, phi_ref, gBD = wd_point
+                f, d, gf, J = df * ev.F, dc * ev.g, df * ev.gradF, dc[:, None] * ev.J
+                in_wd, wd_cnt, tiny = False, 0, False
+            if wd_trigger > 0 and not in_wd and not tiny and not in_soft_resto and wd_cnt >= wd_trigger:
+                # StartWatchDog: store the iterate, its step and the reference values
+                wd_point = (x, s, y, zl, zu, vl, vu, ev, step, theta_ref, phi_ref, gBD)
+                wd_alpha = frac_to_bound(tau, x, s, dx, ds)
+                wd_trial, in_wd = 0, True
+                self.wd_events["start"] += 1
+            if in_wd:  # FilterLSAcceptor::InitThisLineSearch(in_watchdog)
+                theta_ref, phi_ref, gBD = wd_point[9], wd_point[10], wd_point[11]
+            wd_forced = False
             if in_soft_resto:
                 soft_resto_counter += 1
                 if soft_resto_counter <= o["max_soft_resto_iters"]:
@@ -1320,47 +1435,29 @@ class IpoptDense:
                     accepted = ("reg", a, step, tri)
                     tiny_step_flag = True
             else:
-                amin = o["gamma_theta"]
-                if gBD < 0:
-                    amin = min(o["gamma_theta"], o["gamma_phi"] * theta_ref / (-gBD))
-                    if theta_ref <= theta_min:
-                        amin = min(amin, o["delta"] * theta_ref ** o["s_theta"] / (-gBD) ** o["s_phi"])
-                amin *= o["alpha_min_frac"]
-                amax_p = frac_to_bound(tau, x, s, dx, ds)
-                a = amax_p
-                n_steps = 0
-                while a > amin or n_steps == 0:
-                    ls_trials += 1
-                    tri = trial(a, dx, ds)
-                    if tri is not None and check_accept(a, tri[5], tri[6]):
-                        accepted = ("reg", a, step, tri)
+                skip_first = False
+                while True:
+                    accepted, n_steps, ntr, soc_taken, a_test, ev_err, wtri = line_search(skip_first)
+                    ls_trials += ntr
+                    if not in_wd:
                         break
-                    if tri is not None and a == amax_p and theta_ref <= tri[6] and o["max_soc"] > 0:
-                        # second-order correction (FilterLSAcceptor::TrySecondOrderCorrection)
-                        th_tr = tri[6]
-                        th_old = 0.0
-                        a_soc = a
-                        dms = rd.copy()
-                        cnt = 0
-                        cur = tri
-                        while cnt < o["max_soc"] and (cnt == 0 or th_tr <= o["kappa_soc"] * th_old):
-                            th_old = th_tr
-                            dms = a_soc * dms + (cur[4] - cur[1])
-                            stp = solve_dir(dms)
-                            a_soc = frac_to_bound(tau, x, s, stp[0], stp[1])
-                            cur = trial(a_soc, stp[0], stp[1])
-                            if cur is None:
-                                break
-                            if check_accept(a, cur[5], cur[6]):
-                                accepted = ("reg", a_soc, stp, cur)
-                                soc_taken = True
-                                break
-                            cnt += 1
-                            th_tr = cur[6]
-                        if accepted is not None:
-                            break
-                    a *= o["alpha_red_factor"]
-                    n_steps += 1
+                    if accepted is not None:  # watchdog procedure successful
+                        in_wd = False
+                        self.wd_events["success"] += 1
+                        break
+                    wd_trial += 1
+                    if ev_err or wd_trial > wd_max:
+                        # StopWatchDog: back to the stored point and step, then a regular
+                        # backtracking search on it that skips the (already rejected) full step
+                        x, s, y, zl, zu, vl, vu, ev, step, theta_ref, phi_ref, gBD = wd_point
+                        f, d, gf, J = df * ev.F, dc * ev.g, df * ev.gradF, dc[:, None] * ev.J
+                        in_wd, wd_cnt, skip_first = False, 0, True
+                        self.wd_events["stop"] += 1
+                        continue
+                    # a watchdog trial iteration: the full step is taken unchecked
+                    accepted = ("reg", frac_to_bound(tau, x, s, step[0], step[1]), step, wtri)
+                    wd_forced = True
+                    break
                 if accepted is None:
                     r = try_soft_resto(step)
                     if r is not None:
@@ -1368,11 +1465,13 @@ class IpoptDense:
                         if not r[-1]:
                             in_soft_resto = True
                             soft_resto_counter = 0
-                elif accepted[0] == "reg":
-                    a_test = a
+                elif not wd_forced:
                     phi_acc = accepted[3][5]
                     if not (is_ftype(a_test) and armijo(a_test, phi_acc)):
                         filt.append((phi_ref - o["gamma_phi"] * theta_ref, (1.0 - o["gamma_theta"]) * theta_ref))
+            if accepted is not None and accepted[0] == "reg":
+                # successive shortened steps trigger the watchdog
+                wd_cnt = 0 if n_steps == 0 else wd_cnt + 1
 
             if accepted is None:
                 # feasibility restoration phase (BacktrackingLineSearch -> RestoMinC_1Nrm)
@@ -1394,6 +1493,7 @@ class IpoptDense:
                 x, s, ev, y, zl, zu, vl, vu = (rres[k] for k in ("x", "s", "ev", "y", "zl", "zu", "vl", "vu"))
                 f, d = df * ev.F, dc * ev.g
                 in_soft_resto = False
+                wd_cnt = 0
                 accepted = ("resto",)
 
             if accepted[0] == "reg":

@@ -233,7 +233,11 @@ def test_full_size_properties():
         ev = orc.SSEval(prob, a["x"][:, i], P[i])
         stat = ev.gradF + ev.J.T @ a["lam_g"][:, i] + a["lam_x"][:, i]
         assert np.max(np.abs(stat)) <= 1e-6 * (1 + np.max(np.abs(ev.gradF)))
-        assert np.all(ev.g <= ubg + 1e-6) and np.all(ev.g >= lbg - 1e-6)
+        # Solve_Succeeded means a constraint violation <= constr_viol_tol = 1e-4 (IPOPT's
+        # unscaled test) against the bounds relaxed by bound_relax_factor = 1e-8
+        viol = max(float(np.max(ev.g - ubg)), float(np.max(lbg - ev.g)), 0.0)
+        print(f"scenario {i}: max bound violation {viol:.3e}")
+        assert viol <= 1e-4
 
 
 def test_device_path_matches_host_path():

@@ -1,0 +1,138 @@
+"""GPU parity against the oracle's closed-loop fixtures (tests/golden/gen_closed_loop.py):
+BASELINE config 3 (the bench's workload: N=20, 10 obstacles, 64 scenarios x 20
+warm-started MPC steps) and config 5 (N=50, dynamic obstacles moving per
+MATLAB/Dynamic Obstacles/Dynamic Obstacle avoidance.m:213-230; 16 cold solves and
+16 scenarios x 10 warm-started steps).
+
+Two comparisons per case:
+  * per step: the HIP solver on exactly the (w, p) the oracle saw at every step,
+    so no earlier difference propagates -- status, iteration count, and x / f at
+    the north-star tolerance |a - b| <= 1e-6 (1 + |b|);
+  * chained: nmpc_closed_loop_dev from the fixture's start, compared step by step
+    (status, u0, f) until the two loops first disagree.
+Mismatches are printed; the thresholds below are what the test enforces.
+"""
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+TOL = 1e-6
+
+
+def _load(name):
+    path = os.path.join(GOLD, f"closed_loop_{name}.npz")
+    if not os.path.exists(path):
+        pytest.fail(f"missing fixture {path} (python tests/golden/gen_closed_loop.py {name})")
+    return np.load(path)
+
+
+def _solver(cfg):
+    from nmpc_amd import nlpsol, config_spec, REFERENCE_OPTS
+
+    spec = config_spec(cfg)
+    return spec, nlpsol("solver", "ipopt", spec, REFERENCE_OPTS)
+
+
+def _relerr(a, b):
+    return np.max(np.abs(a - b) / (1.0 + np.abs(b)), axis=-1)
+
+
+def _per_step(name):
+    z = _load(name)
+    spec, s = _solver(int(z["cfg"]))
+    lbx, ubx, lbg, ubg = spec.bounds()
+    W = z["w"].reshape(-1, spec.nw)
+    Pp = z["p"].reshape(-1, spec.np)
+    sol = s(x0=W.T, lbx=lbx, ubx=ubx, lbg=lbg, ubg=ubg, p=Pp.T)
+    st, it = s.stats()["status_code"], s.stats()["iter_count"]
+    ost, oit = z["status"].ravel(), z["iter"].ravel()
+    ox, of = z["x"].reshape(-1, spec.nw), z["f"].ravel()
+    same = st == ost
+    conv = same & np.isin(ost, (0, 1))
+    ex = _relerr(sol["x"].T, ox)
+    ef = np.abs(sol["f"][0] - of) / (1 + np.abs(of))
+    ok_x = conv & (ex <= TOL) & (ef <= TOL)
+    print(f"\n{name} per step: {len(ost)} solves; status agree {same.mean():.4f}; iterations agree "
+          f"{(it == oit).mean():.4f}; converged+agreeing {conv.sum()}, within 1e-6 {ok_x.sum()}; "
+          f"oracle statuses {dict(zip(*np.unique(ost, return_counts=True)))}")
+    for i in np.flatnonzero(~same | (conv & ~ok_x))[:12]:
+        print(f"  step {i}: gpu status {st[i]} it {it[i]} | oracle status {ost[i]} it {oit[i]} | "
+              f"x rel err {ex[i]:.2e} f rel err {ef[i]:.2e}")
+    return same, conv, ok_x, it == oit
+
+
+@pytest.mark.parametrize("name", ["config3", "config5"])
+def test_per_step_parity_with_oracle_fixture(name):
+    same, conv, ok_x, same_it = _per_step(name)
+    assert same.mean() >= 0.95
+    assert ok_x.sum() >= 0.95 * conv.sum()
+    assert same_it.mean() >= 0.90
+
+
+def test_config5_cold_solves_match_oracle():
+    """N=50 cold starts (u = 0, Python/NMPC_TT.py:329): the oracle's status mix,
+    including its max-iterations share, is reproduced solve by solve."""
+    z = _load("config5")
+    spec, s = _solver(5)
+    lbx, ubx, lbg, ubg = spec.bounds()
+    n = len(z["cold_status"])
+    sol = s(x0=np.zeros(spec.nw), lbx=lbx, ubx=ubx, lbg=lbg, ubg=ubg, p=z["P"][:n].T)
+    st, it = s.stats()["status_code"], s.stats()["iter_count"]
+    print(f"\nconfig5 cold: gpu {dict(zip(*np.unique(st, return_counts=True)))} "
+          f"oracle {dict(zip(*np.unique(z['cold_status'], return_counts=True)))}; "
+          f"iterations agree {(it == z['cold_iter']).mean():.3f}")
+    assert (st == z["cold_status"]).mean() >= 15 / 16
+    conv = (st == z["cold_status"]) & np.isin(st, (0, 1))
+    if conv.any():
+        assert np.all(_relerr(sol["x"].T[conv], z["cold_x"][conv]) <= TOL)
+
+
+@pytest.mark.parametrize("name", ["config3", "config5"])
+def test_chained_closed_loop_matches_oracle_fixture(name):
+    import torch
+
+    z = _load(name)
+    spec, s = _solver(int(z["cfg"]))
+    B, K = z["status"].shape
+    f64 = dict(dtype=torch.float64, device="cuda")
+    bnd = [torch.tensor(v, **f64) for v in spec.bounds()]
+    p = torch.tensor(z["P"], **f64)
+    w = torch.zeros(B, spec.nw, **f64)
+    vt, wt = torch.full((B,), float(z["vt"]), **f64), torch.full((B,), float(z["wt"]), **f64)
+    hist = {"u": torch.empty(K, B, 6, **f64), "f": torch.empty(K, B, **f64),
+            "status": torch.empty(K, B, dtype=torch.int32, device="cuda"),
+            "iters": torch.empty(K, B, dtype=torch.int32, device="cuda")}
+    s.closed_loop_device(K, *bnd, p, w, vt, wt, hist, p_step=torch.tensor(z["p_step"], **f64))
+    torch.cuda.synchronize()
+    H = {k: v.cpu().numpy() for k, v in hist.items()}
+    nu = spec.nu
+    matched, total, full = 0, B * K, 0
+    for b in range(B):
+        ok_chain = True
+        for k in range(K):
+            o_u = z["x"][b, k, :nu]
+            g_u = H["u"][k, b, :nu]
+            conv = z["status"][b, k] in (0, 1)
+            ok = (H["status"][k, b] == z["status"][b, k] and
+                  (not conv or (np.max(np.abs(g_u - o_u) / (1 + np.abs(o_u))) <= TOL and
+                                abs(H["f"][k, b] - z["f"][b, k]) <= TOL * (1 + abs(z["f"][b, k])))))
+            if not ok:
+                eu = np.max(np.abs(g_u - o_u) / (1 + np.abs(o_u)))
+                ef = abs(H["f"][k, b] - z["f"][b, k]) / (1 + abs(z["f"][b, k]))
+                print(f"  scenario {b} diverges at step {k}: gpu status {H['status'][k, b]} it {H['iters'][k, b]}"
+                      f" | oracle {z['status'][b, k]} it {z['iter'][b, k]} | u0 rel err {eu:.2e}, f rel err {ef:.2e}")
+                ok_chain = False
+                break
+            matched += 1
+        full += ok_chain
+    print(f"\n{name} chained: {full}/{B} chains identical over {K} steps; {matched}/{total} steps before "
+          f"the first divergence")
+    # the device loop's shift (fused multiply-adds) and numpy's differ by rounding; near a
+    # termination threshold that can change an iteration count and the chain from there
+    # on, so chains are required to agree up to their first divergence on 90% of the
+    # steps (the per-step test above compares every step from identical inputs)
+    assert matched >= 0.9 * total
+    assert full >= 0.75 * B
