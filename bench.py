@@ -160,7 +160,7 @@ def main():
     import torch
     import torch.distributed as dist
     from nmpc_amd import nlpsol, config_spec, draw_scenarios, REFERENCE_OPTS
-    from nmpc_amd.dist import shard, pack_result, gather_rows
+    from nmpc_amd.dist import shard, pack_result, gather_rows, gather_closed_loop
     from nmpc_amd.schedule import longest_first
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -225,19 +225,18 @@ def main():
         if not cold:
             solver.shift_device(p, out["x"], w, v_t, w_t, stream=stream)
         if world > 1:  # per-step gather of (u0, f, status)
-            gather_rows(pack_result(out["x"], out["f"], out["status"]), world)
-        hist["u"][k].copy_(out["x"][:, :6]); hist["f"][k].copy_(out["f"])
+            gather_rows(pack_result(out["x"], out["f"], out["status"], spec.nu), world)
+        hist["u"][k].zero_(); hist["u"][k][:, :spec.nu].copy_(out["x"][:, :spec.nu]); hist["f"][k].copy_(out["f"])
         hist["iters"][k].copy_(out["iters"]); hist["status"][k].copy_(out["status"])
 
     def fused(p, w, hist, k_steps, timed_events=None, order=None):
         if timed_events is not None:
             timed_events[0].record(stream)
-        solver.closed_loop_device(k_steps, *bnd, p, w, v_t, w_t, hist, stream=stream, order=order)
+        solver.closed_loop_device(k_steps, *bnd, p, w, v_t, w_t, hist, stream=stream, order=order, check=False)
         if timed_events is not None:
             timed_events[1].record(stream)
         if world > 1:  # the only exchange: final gather of every step's (u0, f, status)
-            gather_rows(torch.cat([hist["u"].permute(1, 0, 2).reshape(B, -1), hist["f"].t(),
-                                   hist["status"].t().double()], dim=1).contiguous(), world)
+            gather_closed_loop(hist, world)
 
     def barrier_sync():
         torch.cuda.synchronize()
@@ -271,6 +270,8 @@ def main():
                 per_step(p, w, ht, k, mode == "cold", evs[k])
         barrier_sync()
         elapsed = time.perf_counter() - t0
+        if mode == "fused":  # every (scenario, step) ran: raises otherwise (after the timed region)
+            timed_run.info = solver.check_closed_loop(B, K)
         kern_ms = [a.elapsed_time(b) for a, b in evs]
         el_t = torch.tensor([elapsed], **f64)
         tot = torch.stack([ht["iters"].sum().double(), torch.tensor(float(B * K), **f64)])
@@ -300,7 +301,7 @@ def main():
         kern_avg_s = float(np.mean(kern_ms)) / 1e3
         steps_per_launch = K if args.mode == "fused" else 1
         kname = "nmpc_closed_loop_kernel" if args.mode == "fused" else "nmpc_solve_kernel"
-        if args.mode == "fused" and solver.closed_loop_info()["policy"] == "step_queues":
+        if args.mode == "fused" and timed_run.info["policy"] == "step_queues":
             kname = "nmpc_closed_loop_sched_kernel"
         flops_launch = B * steps_per_launch * ibar * (spec.N + 1) * KFLOP_PER_STAGE_ITER * 1e3
         achieved_tf = flops_launch / kern_avg_s / 1e12
@@ -337,17 +338,18 @@ def main():
             "status_histogram": status_hist,
         }
         if args.mode == "fused":
-            info = solver.closed_loop_info()
+            info = timed_run.info
             first = ("index order" if (args.in_order or W == 0) else
                      "longest-expected-first by the iterations of the "
                      f"{W} warm-up MPC steps that precede the timed steps (nmpc_amd.schedule)")
             if info["policy"] == "step_queues":
-                res["dispatch"] = (f"step queues: {info['resident_waves']} persistent waves claim (scenario, step) "
+                res["dispatch"] = (f"step queues: {info['launched_waves']} persistent waves claim (scenario, step) "
                                    f"pairs whose previous step is done, lowest step first, scenarios pinned to an "
                                    f"XCD; initial order {first}")
             else:
                 res["dispatch"] = f"one workgroup per scenario, {first}"
             res["scheduler_error"] = info["scheduler_error"]
+            res["steps_done"] = info["steps_done"]
         if fov_mean is not None:
             res["closed_loop_fov_error_mean_m"] = fov_mean  # Python/NMPC_TT.py:433-437 metric, per step
         if side is not None:

@@ -208,16 +208,27 @@ int nmpc_closed_loop_dev(nmpc_handle* h, int32_t B, int32_t K,
                          double* u_hist, double* x_hist, double* f_hist, double* fov_hist,
                          int32_t* status_hist, int32_t* iters_hist, const int32_t* order, void* stream);
 
-/* Scheduling of the last nmpc_closed_loop_dev launch (diagnostics; synchronises the
- * device when sched_err is requested).  policy: 0 = one workgroup per scenario running
- * its K steps back to back (B <= resident waves, or NMPC_CLOSED_LOOP=static);
- * 1 = step queues: persistent waves claim (scenario, step) pairs whose previous step is
- * done, lowest step first, each scenario pinned to one XCD.  resident: waves the
- * closed-loop kernel keeps resident (occupancy x CUs; 0 before the first launch).
- * sched_err: 1 if a wave gave up waiting for a published step (not expected). */
-int nmpc_closed_loop_info(nmpc_handle* h, int32_t* policy, int32_t* resident, int32_t* sched_err);
+/* Scheduling of the last nmpc_closed_loop_dev launch (synchronises the device when
+ * sched_err or steps_done is requested; any pointer may be NULL).
+ *   policy: 0 = one workgroup per scenario running its K steps back to back (B <=
+ *     resident waves, a device without exactly 8 XCDs, or NMPC_CLOSED_LOOP=static);
+ *     1 = step queues: persistent waves claim (scenario, step) pairs whose previous step
+ *     is done, lowest step first, each scenario pinned to one XCD.
+ *   resident: waves the closed-loop kernel keeps resident (occupancy x CUs; 0 before
+ *     the first launch).  waves: workgroups the last launch started.
+ *   sched_err: bit 0 a wave gave up waiting for a published step, bit 1 a scenario did
+ *     not complete its K steps (its unrun steps carry status NMPC_STATUS_NOT_RUN and NaN
+ *     f / u in the histories).  0 on success.
+ *   steps_done: closed-loop steps completed (must equal B*K). */
+#define NMPC_STATUS_NOT_RUN (-1000)
+int nmpc_closed_loop_info(nmpc_handle* h, int32_t* policy, int32_t* resident, int32_t* sched_err,
+                          int32_t* waves, int64_t* steps_done);
 
 const char* nmpc_last_error(void);
+
+/* Hash of the source, header and compile flags the library was built from
+ * (__graft_entry__.source_hash); tests compare it with the checked-out source. */
+const char* nmpc_build_id(void);
 
 /* Launch geometry / workspace of the last solve, for measurement. */
 int nmpc_kernel_info(const nmpc_handle* h, int32_t* lds_bytes, int32_t* threads_per_scenario);

@@ -34,7 +34,10 @@
 
 #include "nmpc_amd.h"
 
-namespace {
+// Named (not anonymous): the library is built as several translation units (one per
+// capacity class, compiled in parallel, plus the host side, NMPC_TU_CLASS / NMPC_TU_HOST)
+// that exchange kernel pointers whose signatures use these types.
+namespace nmpc_impl {
 
 constexpr int WAVE = 64;
 #define LDS __attribute__((address_space(3)))
@@ -3058,8 +3061,12 @@ struct SchedQ {
   int* tail;  // NXCD x K: published count
   int* resv;  // NXCD x K: reserved count
   int* ring;  // NXCD x K x BX scenario ids (-1 = not yet written)
-  int* err;   // 1: a wave gave up waiting
+  int* err;   // [0]: 1 a wave gave up waiting, 2 a scenario did not complete its K steps;
+              // [1]: closed-loop steps completed (nmpc_sched_check_kernel)
+  int* done;  // B: steps completed per scenario
   int BX;     // ring capacity per queue = ceil(B / NXCD)
+  int one_set;  // test hook (NMPC_SCHED_TEST_ONE_SET): only the waves on XCD 0 run, so
+                // sets 1..7 are never drained and the check must report it
 };
 constexpr unsigned long long kSchedWaitTicks = 1000000000ull;  // s_memrealtime (100 MHz): 10 s
 
@@ -3084,6 +3091,7 @@ __global__ __launch_bounds__(WAVE, NMPC_WAVES_PER_EU) void nmpc_closed_loop_sche
   extern __shared__ __attribute__((aligned(16))) double smem[];
   const int K = lp.K;
   const int x = xcc_id();
+  if (q.one_set && x != 0) return;  // test hook: only XCD 0's waves run (sets 1..7 unserved)
   const int nset = (B - x + NXCD - 1) / NXCD;  // scenarios in this XCD's set
   int* head = q.head + x * K;
   int* tail = q.tail + x * K;
@@ -3128,6 +3136,7 @@ __global__ __launch_bounds__(WAVE, NMPC_WAVES_PER_EU) void nmpc_closed_loop_sche
     if (cb >= 0 && cb < B) {  // an out-of-range dispatch entry is claimed and skipped
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // the previous step's p, w (L1 invalidated)
       cl_step<CAP>(prm, B, io, lp, cb, ck, smem);
+      if (threadIdx.x == 0) q.done[cb] = ck + 1;
       stores_done();  // this step's p, w, histories are in the XCD's L2
     }
     if (threadIdx.x == 0 && ck + 1 < K) {
@@ -3142,6 +3151,7 @@ __global__ __launch_bounds__(WAVE, NMPC_WAVES_PER_EU) void nmpc_closed_loop_sche
   }
 }
 
+#ifndef NMPC_TU_CLASS  // host translation unit: the small non-template kernels and the C-ABI
 // queue (x, 0) = the set-x entries of the dispatch order (identity or the caller's
 // permutation); every other queue empty
 __global__ void nmpc_sched_init_kernel(int B, int K, const int* order, SchedQ q) {
@@ -3166,7 +3176,28 @@ __global__ void nmpc_sched_init_kernel(int B, int K, const int* order, SchedQ q)
     q.tail[i] = j == 0 ? nset : 0;
     q.resv[i] = j == 0 ? nset : 0;
   }
-  if (i == 0) q.err[0] = 0;
+  if (i == 0) { q.err[0] = 0; q.err[1] = 0; }
+  if (i < B) q.done[i] = 0;
+}
+
+// After a step-queue launch (same stream): every scenario must have completed its K
+// steps (Python/NMPC_TT.py:348-402 advances every scenario K times).  A scenario that
+// did not sets err[0] |= 2, and its unrun steps are marked in the histories
+// (status NMPC_STATUS_NOT_RUN, f and u NaN) so nothing is left uninitialised.
+__global__ void nmpc_sched_check_kernel(int B, int K, SchedQ q, int* st_hist, double* f_hist, double* u_hist) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  const int d = q.done[b];
+  atomicAdd(q.err + 1, d);
+  if (d == K) return;
+  atomicOr(q.err, 2);
+  for (int k = d < 0 ? 0 : d; k < K; ++k) {
+    const long long kb = (long long)k * B + b;
+    if (st_hist) st_hist[kb] = NMPC_STATUS_NOT_RUN;
+    if (f_hist) f_hist[kb] = __builtin_nan("");
+    if (u_hist)
+      for (int c = 0; c < 6; ++c) u_hist[kb * 6 + c] = __builtin_nan("");
+  }
 }
 
 // closed-loop shift kernel (Python/NMPC_TT.py:13-30): one thread per scenario
@@ -3201,12 +3232,41 @@ int fail(int code, const std::string& msg) {
   g_err = msg;
   return code;
 }
+#endif  // !NMPC_TU_CLASS
 
-}  // namespace
+}  // namespace nmpc_impl
+using namespace nmpc_impl;
 
 typedef void (*KernFn)(const Params*, int, IO);
 typedef void (*LoopFn)(const Params*, int, IO, Loop);
 typedef void (*SchedFn)(const Params*, int, IO, Loop, SchedQ);
+// the kernels of one capacity class (defined in that class's translation unit)
+struct ClassFns {
+  KernFn fn; LoopFn lfn; SchedFn sfn;
+  int lds_doubles, ws_doubles;
+};
+ClassFns nmpc_class_fns_A();
+ClassFns nmpc_class_fns_B();
+ClassFns nmpc_class_fns_C();
+
+using CapA = Cap<20, 15>;   // BASELINE configs 2-4 (N=20, <=10 obstacles) and the reference's N=15 scripts
+using CapB = Cap<31, 21>;
+using CapC = Cap<63, 21>;   // any supported shape
+
+#ifdef NMPC_TU_CLASS
+template <class CAP>
+static ClassFns class_fns() {
+  return {nmpc_solve_kernel<CAP>, nmpc_closed_loop_kernel<CAP>, nmpc_closed_loop_sched_kernel<CAP>, CAP::L.total,
+          CAP::L.wstotal};
+}
+#if NMPC_TU_CLASS == 1
+ClassFns nmpc_class_fns_A() { return class_fns<CapA>(); }
+#elif NMPC_TU_CLASS == 2
+ClassFns nmpc_class_fns_B() { return class_fns<CapB>(); }
+#else
+ClassFns nmpc_class_fns_C() { return class_fns<CapC>(); }
+#endif
+#else  // host translation unit
 
 struct nmpc_handle {
   Params hp;
@@ -3224,8 +3284,11 @@ struct nmpc_handle {
   int resident = 0;            // closed-loop waves resident at once (occupancy x CUs)
   int* dsched = nullptr;       // step-queue scheduler state
   size_t sched_bytes = 0;
+  int nxcc = -1;               // XCDs of the device (hipDeviceAttributeNumberOfXccs)
   int last_policy = 0;         // last closed-loop launch: 0 one workgroup per scenario, 1 step queues
-  int* last_err = nullptr;     // device flag of the last step-queue launch
+  int last_waves = 0;          // workgroups launched by the last closed-loop launch
+  long long last_steps = 0;    // B*K of the last closed-loop launch
+  int* last_err = nullptr;     // device flags of the last step-queue launch (SchedQ::err)
   int ws_doubles = 0;
   bool trace = false;
   double* dtrace = nullptr;
@@ -3235,20 +3298,14 @@ struct nmpc_handle {
   int last_B = 0;
 };
 
-using CapA = Cap<20, 15>;   // BASELINE configs 2-4 (N=20, <=10 obstacles) and the reference's N=15 scripts
-using CapB = Cap<31, 21>;
-using CapC = Cap<63, 21>;   // any supported shape
 
-template <class CAP>
-static void set_class(KernFn* fn, LoopFn* lfn, SchedFn* sfn, int* lds_doubles, int* ws_doubles) {
-  *fn = nmpc_solve_kernel<CAP>; *lfn = nmpc_closed_loop_kernel<CAP>; *sfn = nmpc_closed_loop_sched_kernel<CAP>;
-  *lds_doubles = CAP::L.total; *ws_doubles = CAP::L.wstotal;
-}
 
 static void pick_class(const Params& P, KernFn* fn, LoopFn* lfn, SchedFn* sfn, int* lds_doubles, int* ws_doubles) {
-  if (P.N <= CapA::nmax && P.m <= CapA::mmax) set_class<CapA>(fn, lfn, sfn, lds_doubles, ws_doubles);
-  else if (P.N <= CapB::nmax && P.m <= CapB::mmax) set_class<CapB>(fn, lfn, sfn, lds_doubles, ws_doubles);
-  else set_class<CapC>(fn, lfn, sfn, lds_doubles, ws_doubles);
+  ClassFns c;
+  if (P.N <= CapA::nmax && P.m <= CapA::mmax) c = nmpc_class_fns_A();
+  else if (P.N <= CapB::nmax && P.m <= CapB::mmax) c = nmpc_class_fns_B();
+  else c = nmpc_class_fns_C();
+  *fn = c.fn; *lfn = c.lfn; *sfn = c.sfn; *lds_doubles = c.lds_doubles; *ws_doubles = c.ws_doubles;
 }
 
 static int ensure_ws(nmpc_handle* h, int B) {
@@ -3287,6 +3344,13 @@ void nmpc_default_options(nmpc_options* o) {
 }
 
 const char* nmpc_last_error(void) { return g_err.c_str(); }
+
+#ifndef NMPC_SRC_HASH
+#define NMPC_SRC_HASH "unknown-unknown-unknown-unknown!"
+#endif
+// the marker lets the build read the hash back from the binary without loading it
+__attribute__((used)) static const char kBuildId[] = "NMPC_SRC_HASH=" NMPC_SRC_HASH;
+const char* nmpc_build_id(void) { return kBuildId + 14; }
 
 int nmpc_create(const nmpc_desc* desc, nmpc_handle** out) {
   if (!desc || !out) return fail(NMPC_E_INVALID, "null argument");
@@ -3361,15 +3425,19 @@ int nmpc_create(const nmpc_desc* desc, nmpc_handle** out) {
   return NMPC_OK;
 }
 
-int nmpc_closed_loop_info(nmpc_handle* h, int32_t* policy, int32_t* resident, int32_t* sched_err) {
+int nmpc_closed_loop_info(nmpc_handle* h, int32_t* policy, int32_t* resident, int32_t* sched_err,
+                          int32_t* waves, int64_t* steps_done) {
   if (!h) return fail(NMPC_E_INVALID, "null handle");
   if (policy) *policy = h->last_policy;
   if (resident) *resident = h->resident;
-  if (sched_err) {
-    int e = 0;
-    if (h->last_err && hipMemcpy(&e, h->last_err, sizeof(int), hipMemcpyDeviceToHost) != hipSuccess)
-      return fail(NMPC_E_HIP, "reading the scheduler flag");
-    *sched_err = e;
+  if (waves) *waves = h->last_waves;
+  if (sched_err || steps_done) {
+    int e[2] = {0, 0};
+    if (h->last_err && hipMemcpy(e, h->last_err, 2 * sizeof(int), hipMemcpyDeviceToHost) != hipSuccess)
+      return fail(NMPC_E_HIP, "reading the scheduler flags");
+    if (sched_err) *sched_err = e[0];
+    // one workgroup per scenario runs all K steps of its scenario by construction
+    if (steps_done) *steps_done = h->last_err ? (int64_t)e[1] : (int64_t)h->last_steps;
   }
   return NMPC_OK;
 }
@@ -3554,7 +3622,7 @@ int nmpc_closed_loop_dev(nmpc_handle* h, int32_t B, int32_t K, const double* lbx
   if (ld_tk < 0 || ld_tb < 0) return fail(NMPC_E_INVALID, "negative target-schedule stride");
   if (p_step && ld_ps < 0) return fail(NMPC_E_INVALID, "negative p_step stride");
   const Params& P = h->hp;
-  if ((ld_lbx != 0 && ld_lbx < P.nw) || (ld_ubx != 0 && ld_ubx < P.nw) || (ld_lbg != 0 && ld_lbg < P.ng) ||
+  if ((ld_lbx != 0 && ld_lbx < P.nwE) || (ld_ubx != 0 && ld_ubx < P.nwE) || (ld_lbg != 0 && ld_lbg < P.ng) ||
       (ld_ubg != 0 && ld_ubg < P.ng) || ld_p < P.npE)
     return fail(NMPC_E_INVALID, "leading dimension smaller than the vector length");
   if ((long long)B * K > (1LL << 40)) return fail(NMPC_E_INVALID, "B*K too large");
@@ -3582,11 +3650,21 @@ int nmpc_closed_loop_dev(nmpc_handle* h, int32_t B, int32_t K, const double* lbx
     cus = prop.multiProcessorCount;
     h->resident = per_cu * cus;
   }
+  if (h->nxcc < 0) {
+    int nx = 0;
+    if (hipDeviceGetAttribute(&nx, hipDeviceAttributeNumberOfXccs, h->device) != hipSuccess) nx = 0;
+    h->nxcc = nx;
+  }
   const char* pol = std::getenv("NMPC_CLOSED_LOOP");
-  const bool use_q = (B > h->resident) && h->resident >= NXCD && !(pol && std::strcmp(pol, "static") == 0);
+  // the step queues pin scenarios to XCD sets by the XCC_ID of the running wave: only
+  // valid when the device has exactly the NXCD XCDs the sets assume (SPX mode of an
+  // MI355X); otherwise one workgroup per scenario
+  const bool use_q = (B > h->resident) && h->resident >= NXCD && h->nxcc == NXCD &&
+                     !(pol && std::strcmp(pol, "static") == 0);
+  h->last_steps = (long long)B * K;
   if (use_q) {
     const int BX = (B + NXCD - 1) / NXCD;
-    const size_t nint = (size_t)3 * NXCD * K + (size_t)NXCD * K * BX + 1;
+    const size_t nint = (size_t)3 * NXCD * K + (size_t)NXCD * K * BX + 2 + (size_t)B;
     if (nint * sizeof(int) > h->sched_bytes) {
       if (h->dsched) hipFree(h->dsched);
       h->dsched = nullptr; h->sched_bytes = 0;
@@ -3595,13 +3673,17 @@ int nmpc_closed_loop_dev(nmpc_handle* h, int32_t B, int32_t K, const double* lbx
     }
     SchedQ q;
     q.head = h->dsched; q.tail = q.head + NXCD * K; q.resv = q.tail + NXCD * K;
-    q.ring = q.resv + NXCD * K; q.err = q.ring + (size_t)NXCD * K * BX; q.BX = BX;
+    q.ring = q.resv + NXCD * K; q.err = q.ring + (size_t)NXCD * K * BX; q.done = q.err + 2; q.BX = BX;
+    const char* one = std::getenv("NMPC_SCHED_TEST_ONE_SET");
+    q.one_set = (one && std::atoi(one) != 0) ? 1 : 0;
     const long long n = (long long)NXCD * K * BX;
     const int thr = 256;
     hipLaunchKernelGGL(nmpc_sched_init_kernel, dim3((unsigned)((n + thr - 1) / thr)), dim3(thr), 0,
                        (hipStream_t)stream, (int)B, (int)K, (const int*)order, q);
-    // persistent waves: all resident ones (NMPC_SCHED_WAVES, a diagnostic, launches
-    // fewer: any count >= NXCD is correct since every launched wave is resident)
+    // persistent waves: all resident ones.  NMPC_SCHED_WAVES (a diagnostic) launches
+    // fewer; correctness needs at least one wave on every XCD, which the hardware's
+    // round-robin placement of workgroups over the XCDs gives for any count >= NXCD,
+    // and the check kernel below reports any scenario left unfinished.
     int waves = h->resident;
     if (const char* ev = std::getenv("NMPC_SCHED_WAVES")) {
       const int w = std::atoi(ev);
@@ -3609,10 +3691,14 @@ int nmpc_closed_loop_dev(nmpc_handle* h, int32_t B, int32_t K, const double* lbx
     }
     hipLaunchKernelGGL(h->sched, dim3(waves), dim3(WAVE), h->lds_bytes, (hipStream_t)stream,
                        (const Params*)h->dprm, (int)B, io, lp, q);
+    hipLaunchKernelGGL(nmpc_sched_check_kernel, dim3((B + thr - 1) / thr), dim3(thr), 0, (hipStream_t)stream,
+                       (int)B, (int)K, q, status_hist, f_hist, u_hist);
     h->last_policy = 1;
+    h->last_waves = waves;
     h->last_err = q.err;
   } else {
     h->last_policy = 0;
+    h->last_waves = B;
     h->last_err = nullptr;
     hipLaunchKernelGGL(h->loop, dim3(B), dim3(WAVE), h->lds_bytes, (hipStream_t)stream,
                        (const Params*)h->dprm, (int)B, io, lp);
@@ -3623,3 +3709,4 @@ int nmpc_closed_loop_dev(nmpc_handle* h, int32_t B, int32_t K, const double* lbx
 }
 
 }  // extern "C"
+#endif  // NMPC_TU_CLASS

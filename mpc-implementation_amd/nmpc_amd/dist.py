@@ -17,11 +17,16 @@ def shard(total: int, world: int, rank: int) -> slice:
     return slice(lo, lo + base + (1 if rank < rem else 0))
 
 
-def pack_result(x, f, status):
-    """(B, 8) float64 rows: u0 (first control column), f, status."""
+def pack_result(x, f, status, nu: int = 6):
+    """(B, 8) float64 rows: u0 (the first nu entries of x, the first control column,
+    zero-padded to 6 like the closed loop's u history), f, status.  nu = 3 for the
+    no-gimbal model, whose x holds 3 controls per stage."""
     import torch
 
-    return torch.cat([x[:, :6], f[:, None], status[:, None].to(x.dtype)], dim=1).contiguous()
+    u0 = x[:, :nu]
+    if nu < 6:
+        u0 = torch.cat([u0, torch.zeros(x.shape[0], 6 - nu, dtype=x.dtype, device=x.device)], dim=1)
+    return torch.cat([u0, f[:, None], status[:, None].to(x.dtype)], dim=1).contiguous()
 
 
 def gather_rows(local, world: int, group=None):
@@ -38,3 +43,19 @@ def gather_rows(local, world: int, group=None):
         dist.all_gather(parts, host, group=group)
         out.copy_(torch.cat(parts, dim=0))
     return out
+
+
+def pack_closed_loop(hist):
+    """(B, 8K) float64 rows of a fused closed-loop launch's histories: every step's u0
+    (6), f and status, scenario-major -- the per-scenario record rank 0 needs."""
+    import torch
+
+    u, f, st = hist["u"], hist["f"], hist["status"]
+    B = u.shape[1]
+    return torch.cat([u.permute(1, 0, 2).reshape(B, -1), f.t(), st.t().to(u.dtype)], dim=1).contiguous()
+
+
+def gather_closed_loop(hist, world: int, group=None):
+    """The fused mode's only exchange: one all-gather of every rank's packed
+    histories after its K-step launch -> (world*B, 8K) on every rank."""
+    return gather_rows(pack_closed_loop(hist), world, group)

@@ -36,6 +36,7 @@ RETURN_STATUS = {
     -11: "Invalid_Problem_Definition", -13: "Invalid_Number_Detected",
 }
 _SUCCESS = (0, 1)
+NOT_RUN = -1000  # NMPC_STATUS_NOT_RUN: a closed-loop step the scheduler never ran
 _DP = C.POINTER(C.c_double)
 _IP = C.POINTER(C.c_int32)
 
@@ -224,7 +225,7 @@ class Solver:
                                     C.c_void_p(stream.cuda_stream)))
 
     def closed_loop_device(self, K: int, lbx, ubx, lbg, ubg, p, w, v_t, w_t, hist: dict | None = None,
-                           stream=None, p_step=None, order=None):
+                           stream=None, p_step=None, order=None, check: bool = True):
         """K closed-loop MPC steps per scenario in one launch (see nmpc_closed_loop_dev).
 
         p (B,np) and w (B,nw) are advanced in place.  Target controls v_t, w_t:
@@ -235,6 +236,9 @@ class Solver:
         obstacles, targets.obstacle_steps).
         ``order`` (B,) int32 device tensor, optional: dispatch order, a permutation
         of range(B) (schedule.longest_first); results do not depend on it.
+        ``check`` (default): synchronise and raise unless every scenario completed its K
+        steps (check_closed_loop); pass False to stay asynchronous and call
+        check_closed_loop later.
         """
         import torch
 
@@ -291,6 +295,8 @@ class Solver:
                                           op("f"), op("fov"), op("status"), op("iters"),
                                           C.c_void_p(order.data_ptr() if order is not None else 0),
                                           C.c_void_p(stream.cuda_stream)))
+        if check:
+            self.check_closed_loop(B, K)
 
     def set_trace(self, enable: bool):
         _lib.check(_lib.lib().nmpc_set_trace(self._h, int(enable)))
@@ -301,11 +307,22 @@ class Solver:
         return buf
 
     def closed_loop_info(self):
-        """Scheduling of the last closed_loop_device launch (nmpc_closed_loop_info)."""
-        pol, res, err = C.c_int32(), C.c_int32(), C.c_int32()
-        _lib.check(_lib.lib().nmpc_closed_loop_info(self._h, C.byref(pol), C.byref(res), C.byref(err)))
+        """Scheduling of the last closed_loop_device launch (nmpc_closed_loop_info;
+        synchronises the device)."""
+        pol, res, err, wav, done = C.c_int32(), C.c_int32(), C.c_int32(), C.c_int32(), C.c_int64()
+        _lib.check(_lib.lib().nmpc_closed_loop_info(self._h, C.byref(pol), C.byref(res), C.byref(err),
+                                                    C.byref(wav), C.byref(done)))
         return {"policy": ("step_queues" if pol.value == 1 else "per_scenario"), "resident_waves": res.value,
-                "scheduler_error": err.value}
+                "launched_waves": wav.value, "scheduler_error": err.value, "steps_done": done.value}
+
+    def check_closed_loop(self, B: int, K: int):
+        """Raise if the last closed-loop launch did not run every (scenario, step)."""
+        info = self.closed_loop_info()
+        if info["scheduler_error"] != 0 or info["steps_done"] != B * K:
+            raise _lib.NmpcError(f"closed loop incomplete: {info['steps_done']} of {B * K} steps run, "
+                                 f"scheduler_error={info['scheduler_error']} (unrun steps carry status "
+                                 f"{NOT_RUN} in the history)")
+        return info
 
     def kernel_info(self):
         lds, tps = C.c_int32(), C.c_int32()

@@ -423,6 +423,7 @@ def test_closed_loop_step_queues_match_per_scenario_dispatch():
         got, p_got, w_got = run(order)
         info = s.closed_loop_info()
         assert info["policy"] == "step_queues" and info["scheduler_error"] == 0, info
+        assert info["steps_done"] == B * K and info["launched_waves"] == res, info
         for k in ref:
             np.testing.assert_array_equal(got[k], ref[k], err_msg=k)
         np.testing.assert_array_equal(p_got, p_ref)
@@ -509,7 +510,7 @@ def test_restoration_phase_against_oracle():
         assert int(st[b]) in (0, 1, 2, -1, -2), int(st[b])
         agree += int(st[b]) == int(G["status"][b])
     print(f"restoration cases: final status agrees with the oracle on {agree}/{B}")
-    assert agree >= B // 2
+    assert agree >= B - 1  # 15/16 at the last run: one case decided at rounding level (docstring)
 
 
 def test_weights_from_p_match_oracle_and_constant_solver():
@@ -677,3 +678,62 @@ def test_no_gimbal_closed_loop_matches_oracle_loop():
     assert checked >= B
 
 
+
+
+def test_no_gimbal_closed_loop_per_scenario_bounds():
+    """Per-scenario (B, 3N) bounds for the no-gimbal model's closed loop (the caller
+    layout's stride is 3N): accepted, and bitwise equal to the shared-bound run."""
+    import torch
+    from nmpc_amd import make_spec
+
+    N, B, K = 10, 4, 2
+    spec = make_spec(None, N=N, T=0.2, model="uav5")
+    P, bnd, vt, wt = _closed_loop_inputs(spec, B, 1001)
+    f64 = dict(dtype=torch.float64, device="cuda")
+    s = _solver(spec)
+    outs = []
+    for per in (False, True):
+        b = [t.expand(B, -1).contiguous() if per else t for t in bnd]
+        p = torch.tensor(P, **f64)
+        w = torch.zeros(B, spec.nw, **f64)
+        hist = {"u": torch.empty(K, B, 6, **f64), "status": torch.empty(K, B, dtype=torch.int32, device="cuda")}
+        s.closed_loop_device(K, *b, p, w, vt, wt, hist)
+        outs.append({k: v.cpu().numpy() for k, v in hist.items()} | {"w": w.cpu().numpy()})
+    for k in outs[0]:
+        np.testing.assert_array_equal(outs[0][k], outs[1][k], err_msg=k)
+
+
+def test_step_queue_guard_reports_unrun_scenarios():
+    """If the XCD sets were not all served (a partitioned device, a CU-masked stream),
+    the step queues would leave scenarios unrun.  NMPC_SCHED_TEST_ONE_SET forces that
+    (only the waves on XCD 0 run, so sets 1..7 have no wave): the launch must raise,
+    never return garbage, and
+    the unrun steps carry NMPC_STATUS_NOT_RUN and NaN in the histories."""
+    import torch
+    from nmpc_amd import make_spec
+    from nmpc_amd._lib import NmpcError
+    from nmpc_amd.nlpsol import NOT_RUN
+
+    spec = make_spec("race_track_2", N=6, T=0.2)
+    s = _solver(spec)
+    f64 = dict(dtype=torch.float64, device="cuda")
+    P0, bnd, vt0, wt0 = _closed_loop_inputs(spec, 8, 5)
+    s.closed_loop_device(1, *bnd, torch.tensor(P0, **f64), torch.zeros(8, spec.nw, **f64), vt0, wt0)
+    B, K = s.closed_loop_info()["resident_waves"] + 64, 2
+    P, bnd, vt, wt = _closed_loop_inputs(spec, B, 11)
+    hist = {"u": torch.zeros(K, B, 6, **f64), "f": torch.zeros(K, B, **f64),
+            "status": torch.full((K, B), 99, dtype=torch.int32, device="cuda")}
+    os.environ["NMPC_SCHED_TEST_ONE_SET"] = "1"
+    try:
+        with pytest.raises(NmpcError, match="closed loop incomplete"):
+            s.closed_loop_device(K, *bnd, torch.tensor(P, **f64), torch.zeros(B, spec.nw, **f64), vt, wt, hist)
+    finally:
+        del os.environ["NMPC_SCHED_TEST_ONE_SET"]
+    info = s.closed_loop_info()
+    assert info["policy"] == "step_queues" and info["scheduler_error"] & 2
+    st = hist["status"].cpu().numpy()
+    pos = np.arange(B)  # dispatch position = scenario index (no order): set = position mod 8
+    assert np.all(st[:, pos % 8 != 0] == NOT_RUN)
+    assert np.all(st[:, pos % 8 == 0] != NOT_RUN) and np.all(st != 99)
+    assert np.isnan(hist["f"].cpu().numpy()[:, pos % 8 != 0]).all()
+    assert info["steps_done"] == K * int((pos % 8 == 0).sum())

@@ -1,0 +1,80 @@
+"""GPU test of bench.py's multi-rank fused path at world size 2 (gloo, both ranks on
+cuda:0): each rank runs nmpc_closed_loop_dev on its contiguous shard of the global
+scenario stream, then the single exchange of the fused mode (dist.gather_closed_loop,
+an all-gather of every step's u0, f and status) assembles the whole batch.  The
+gathered rows must equal a single-rank launch over the whole batch bitwise: results
+do not depend on the GPU count (SURVEY 8(e), weak scaling by scenario shards)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+TOTAL, K = 96, 3
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _closed_loop(P, K):
+    import torch
+    from nmpc_amd import nlpsol, config_spec, REFERENCE_OPTS
+
+    spec = config_spec(3)
+    s = nlpsol("solver", "ipopt", spec, REFERENCE_OPTS)
+    f64 = dict(dtype=torch.float64, device="cuda")
+    B = P.shape[0]
+    bnd = [torch.tensor(v, **f64) for v in spec.bounds()]
+    hist = {"u": torch.empty(K, B, 6, **f64), "f": torch.empty(K, B, **f64),
+            "status": torch.empty(K, B, dtype=torch.int32, device="cuda")}
+    s.closed_loop_device(K, *bnd, torch.tensor(P, **f64), torch.zeros(B, spec.nw, **f64),
+                         torch.full((B,), 12.0, **f64), torch.full((B,), 0.01, **f64), hist)
+    return hist
+
+
+def _rank(rank, world, port, q):
+    import sys
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "mpc-implementation_amd"))
+    import torch
+    import torch.distributed as dist
+    from nmpc_amd import config_spec, draw_scenarios
+    from nmpc_amd.dist import shard, gather_closed_loop
+
+    torch.cuda.set_device(0)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    P_all = draw_scenarios(config_spec(3), TOTAL, seed=1003)
+    hist = _closed_loop(P_all[shard(TOTAL, world, rank)], K)
+    rows = gather_closed_loop(hist, world)
+    if rank == 0:
+        q.put(rows.cpu().numpy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_rank_fused_gather_equals_single_rank():
+    import torch.multiprocessing as mp
+    from nmpc_amd import config_spec, draw_scenarios
+    from nmpc_amd.dist import pack_closed_loop
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rank, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    ref = pack_closed_loop(_closed_loop(draw_scenarios(config_spec(3), TOTAL, seed=1003), K)).cpu().numpy()
+    assert got.shape == ref.shape == (TOTAL, 8 * K)
+    np.testing.assert_array_equal(got, ref)

@@ -69,6 +69,16 @@ def test_library_exports_every_header_symbol():
         assert hasattr(L, name), name
 
 
+def test_library_built_from_this_source():
+    """The shared object under test was compiled from the checked-out kernel source,
+    header and flags (hash embedded at build time, __graft_entry__.source_hash)."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("graft_entry", os.path.join(ROOT, "__graft_entry__.py"))
+    ge = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(ge)
+    assert _lib.lib().nmpc_build_id().decode() == ge.source_hash()
+
+
 def test_struct_layout_matches_header(tmp_path):
     src = tmp_path / "sz.c"
     src.write_text('#include "nmpc_amd.h"\n#include <stdio.h>\n#include <stddef.h>\n'
