@@ -31,6 +31,7 @@
 #include <cstdlib>
 #include <mutex>
 #include <string>
+#include <type_traits>
 
 #include "nmpc_amd.h"
 
@@ -81,23 +82,28 @@ struct Lay {
   // LDS
   int X, Xt, dX;
   int trig, qs, lam;
-  int Kc, kf, Rc, P0, P1, pv0, pv1, St;
+  int kf, Rc, P0, P1, pv0, pv1, St;
   int p, ob, inc, red, rvars;
   int total;    // LDS doubles per scenario
   int wstotal;  // global-workspace doubles per scenario
 };
 constexpr int al2(int n) { return (n + 1) & ~1; }
 constexpr int al8(int n) { return (n + 7) & ~7; }
-constexpr Lay make_layout(int N, int m) {
+// lr: the main iteration's hot row vectors (s, y, vl, vu, d, ds, ds2, dc) live in LDS
+// (capacity classes with a small row count: the row passes then never wait on L2 /
+// Infinity-Cache latency); otherwise in the global workspace
+constexpr Lay make_layout(int N, int m, bool lr) {
   Lay L{};
   const int nw = 6 * N, ng = m * (N + 1), nX = 8 * (N + 1), NS = N + 1;
   int g = 0, o = 0;
   L.U = g; g += al8(nw); L.Ut = g; g += al8(nw); L.dU = g; g += al8(nw); L.dU2 = g; g += al8(nw);
   L.zl = g; g += al8(nw); L.zu = g; g += al8(nw); L.xl = g; g += al8(nw); L.xu = g; g += al8(nw);
   L.sigx = g; g += al8(nw); L.ru = g; g += al8(nw);
-  L.s = g; g += al8(ng); L.y = g; g += al8(ng); L.vl = g; g += al8(ng); L.vu = g; g += al8(ng);
-  L.d = g; g += al8(ng); L.dt = g; g += al8(ng); L.ds = g; g += al8(ng); L.ds2 = g; g += al8(ng);
-  L.dc = g; g += al8(ng); L.dms = g; g += al8(ng);
+  if (!lr) {
+    L.s = g; g += al8(ng); L.y = g; g += al8(ng); L.vl = g; g += al8(ng); L.vu = g; g += al8(ng);
+    L.d = g; g += al8(ng); L.ds = g; g += al8(ng); L.ds2 = g; g += al8(ng); L.dc = g; g += al8(ng);
+  }
+  L.dt = g; g += al8(ng); L.dms = g; g += al8(ng);
   L.filt = g; g += al8(2 * FCAP + 2);
   L.gl = g; g += al8(8 * NS); L.Hl = g; g += al8(21 * NS); L.Qs = g; g += al8(36 * NS);
   L.K = g; g += al8(48 * N); L.Rk = g; g += al8(21 * N);
@@ -115,27 +121,36 @@ constexpr Lay make_layout(int N, int m) {
   L.wstotal = g;
   L.X = o; o += al2(nX); L.Xt = o; o += al2(nX); L.dX = o; o += al2(nX);
   L.trig = o; o += al2(8 * NS); L.qs = o; o += al2(10 * NS); L.lam = o; o += al2(8 * NS);
-  L.Kc = o; o += 48; L.kf = o; o += al2(6 * N); L.Rc = o; o += 22;
+  L.kf = o; o += al2(6 * N); L.Rc = o; o += 22;
   L.P0 = o; o += 64; L.P1 = o; o += 64; L.pv0 = o; o += 8; L.pv1 = o; o += 8; L.St = o; o += 48;
   L.p = o; o += 64; L.ob = o; o += al2(2 * NMPC_MAX_OBS); L.inc = o; o += al2(8 * NS); L.red = o; o += 24;
   L.dl = o; o += al2(ng); L.du = o; o += al2(ng);  // row bounds (constant during a solve, read by every row pass)
   L.rvars = o; o += 48;  // line-search / restoration scalars; [32..36] barrier sums; [40..45] watchdog
+  if (lr) {
+    L.s = o; o += al2(ng); L.y = o; o += al2(ng); L.vl = o; o += al2(ng); L.vu = o; o += al2(ng);
+    L.d = o; o += al2(ng); L.ds = o; o += al2(ng); L.ds2 = o; o += al2(ng); L.dc = o; o += al2(ng);
+  }
   L.total = o;
   return L;
 }
-template <int NMAX, int MMAX>
-struct Cap {
-  static constexpr int nmax = NMAX, mmax = MMAX;
-  static constexpr Lay L = make_layout(NMAX, MMAX);
-  // row passes: trips of 64 rows processed together (their loads batched), <= 5
-  static constexpr int rtrips = (MMAX * (NMAX + 1) + 63) / 64;
-  static constexpr int ru = rtrips < 2 ? rtrips : 2;
-};
-
 // waves per SIMD the kernels are register-budgeted for (256 VGPRs at 2)
 #ifndef NMPC_WAVES_PER_EU
 #define NMPC_WAVES_PER_EU 2
 #endif
+
+// LDSR: hot row vectors in LDS (make_layout); such a class needs ~39 KB of LDS per
+// scenario, so it runs one wave per SIMD (four per CU) with the full 512-VGPR budget
+template <int NMAX, int MMAX, bool LDSR = false>
+struct Cap {
+  static constexpr int nmax = NMAX, mmax = MMAX;
+  static constexpr bool lds_rows = LDSR;
+  static constexpr int wpe = LDSR ? 1 : NMPC_WAVES_PER_EU;
+  using RowT = std::conditional_t<LDSR, LDS double, GLB double>;
+  static constexpr Lay L = make_layout(NMAX, MMAX, LDSR);
+  // row passes: trips of 64 rows processed together (their loads batched), <= 5
+  static constexpr int rtrips = (MMAX * (NMAX + 1) + 63) / 64;
+  static constexpr int ru = rtrips < 2 ? rtrips : 2;
+};
 
 struct IO {
   const double *x0, *lbx, *ubx, *lbg, *ubg, *p;
@@ -305,7 +320,9 @@ struct Solver {
   // pointers into LDS
   GLB double* U, *Ut, *dU, *dU2, *zl, *zu, *xl, *xu, *sigx, *ru;
   LDS double* X, *Xt, *dX;
-  GLB double* s, *y, *vl, *vu, *d, *dt, *ds, *ds2, *dc, *dms;
+  using RV = typename CAP::RowT;  // hot row vectors: LDS or global (Cap::lds_rows)
+  RV *s, *y, *vl, *vu, *d, *ds, *ds2, *dc;
+  GLB double *dt, *dms;
   GLB double *UR, *zl0, *zu0, *s0, *vl0, *vu0, *pR, *nR, *zpR, *znR, *dpR, *dnR, *dyR, *dp2R, *dn2R, *dy2R, *cms, *filtR;
   GLB double *accU, *accZl, *accZu, *accY;
   GLB double *wU, *wzl, *wzu, *wdU, *wsl, *wy, *wvl, *wvu, *wds, *wpR, *wnR, *wzpR, *wznR, *wdpR, *wdnR, *wdyR;
@@ -315,7 +332,7 @@ struct Solver {
   GLB double* gl, *Hl, *Qs;
   LDS double* trig, *qs, *lam;
   GLB double* K, *Rk;
-  LDS double* Kc, *kf, *Rc, *Pa, *Pb, *pva, *pvb, *St;
+  LDS double* kf, *Rc, *Pa, *Pb, *pva, *pvb, *St;
   LDS double* pp, *obx, *oby, *inc, *stamps;
   GLB double* filt;
   // uniform scalars
@@ -334,9 +351,13 @@ struct Solver {
     zl = gw + L.zl; zu = gw + L.zu; xl = gw + L.xl; xu = gw + L.xu;
     sigx = gw + L.sigx; ru = gw + L.ru;
     X = sm + L.X; Xt = sm + L.Xt; dX = sm + L.dX;
-    s = gw + L.s; y = gw + L.y; vl = gw + L.vl; vu = gw + L.vu;
-    d = gw + L.d; dt = gw + L.dt; ds = gw + L.ds; ds2 = gw + L.ds2;
-    dc = gw + L.dc; dl = sm + L.dl; du = sm + L.du; dms = gw + L.dms; rvars = sm + L.rvars;
+    auto rvp = [&](int off) -> RV* {
+      if constexpr (CAP::lds_rows) return (RV*)(sm + off);
+      else return (RV*)(gw + off);
+    };
+    s = rvp(L.s); y = rvp(L.y); vl = rvp(L.vl); vu = rvp(L.vu);
+    d = rvp(L.d); dt = gw + L.dt; ds = rvp(L.ds); ds2 = rvp(L.ds2);
+    dc = rvp(L.dc); dl = sm + L.dl; du = sm + L.du; dms = gw + L.dms; rvars = sm + L.rvars;
     UR = gw + L.UR; zl0 = gw + L.zl0; zu0 = gw + L.zu0; s0 = gw + L.s0; vl0 = gw + L.vl0; vu0 = gw + L.vu0;
     pR = gw + L.pR; nR = gw + L.nR; zpR = gw + L.zpR; znR = gw + L.znR; dpR = gw + L.dpR; dnR = gw + L.dnR;
     dyR = gw + L.dyR; dp2R = gw + L.dp2R; dn2R = gw + L.dn2R; dy2R = gw + L.dy2R; cms = gw + L.cms;
@@ -347,7 +368,7 @@ struct Solver {
     wzpR = gw + L.wzpR; wznR = gw + L.wznR; wdpR = gw + L.wdpR; wdnR = gw + L.wdnR; wdyR = gw + L.wdyR;
     gl = gw + L.gl; Hl = gw + L.Hl; trig = sm + L.trig; Qs = gw + L.Qs; qs = sm + L.qs;
     lam = sm + L.lam;
-    K = gw + L.K; kf = sm + L.kf; Rk = gw + L.Rk; Kc = sm + L.Kc; Rc = sm + L.Rc;
+    K = gw + L.K; kf = sm + L.kf; Rk = gw + L.Rk; Rc = sm + L.Rc;
     Pa = sm + L.P0; Pb = sm + L.P1; pva = sm + L.pv0; pvb = sm + L.pv1;
     St = sm + L.St;
     pp = sm + L.p; obx = sm + L.ob; oby = obx + NMPC_MAX_OBS; inc = sm + L.inc;
@@ -441,7 +462,8 @@ struct Solver {
   }
 
   // f = sum_k l_k(X) and rows dst[r] = dc[r] * g_r(X) (dc may be null -> unscaled)
-  __device__ __forceinline__ double eval_fg(const LDS double* Xs, GLB double* dst, const GLB double* scale) {
+  template <class DP>
+  __device__ __forceinline__ double eval_fg(const LDS double* Xs, DP dst, const RV* scale) {
     STAMP0();
     const int k = lanef();
     double f = 0.0;
@@ -574,7 +596,8 @@ struct Solver {
   // --------------------------------------------- adjoint lam_k (lanef() = k)
   // lam_N = G_N^T y_N; lam_k = ofac*gl_k + G_k^T y_k + A_k^T lam_{k+1}
   // (oracle SSEval.hessian).  yy may be null (objective only).
-  __device__ __forceinline__ void adjoint(double ofac, const GLB double* yy) {
+  template <class YP>
+  __device__ __forceinline__ void adjoint(double ofac, YP yy) {
     STAMP0();
     const int k = lanef();
     LDS double* wv = inc;  // scratch 8*(N+1)
@@ -699,7 +722,7 @@ struct Solver {
     rvars[32] = logs; rvars[33] = damp;
     return phi_of(f, logs, damp);
   }
-  __device__ __forceinline__ double barrier_obj(double f, const GLB double* u, const GLB double* sb, const GLB double* dsv,
+  __device__ __forceinline__ double barrier_obj(double f, const GLB double* u, const RV* sb, const RV* dsv,
                                 double a) {
     STAMP0();
     double logs = 0.0, damp = 0.0;
@@ -725,8 +748,8 @@ struct Solver {
     //     weight dc^2 A (Q part) and right-hand side dc Bw, into scratch row vectors that
     //     are dead in every caller at this point (ds2: SOC step, written after the
     //     solve; dt: trial constraints, rewritten by the next trial)
-    GLB double* Wr = ds2;
-    GLB double* Br = dt;
+    auto Wr = ds2;
+    auto Br = dt;
     rows([&](int r, bool on) {
       const double dcr = dc[r];
       double A, Bw;
@@ -1138,7 +1161,7 @@ struct Solver {
   }
 
   // ds_r = Gt_r dX_k + rd_r (J dU = G Z dU = G dX)
-  __device__ __forceinline__ void row_step(const LDS double* dXs, const GLB double* rdsrc, bool rd_is_dms, GLB double* dso) {
+  __device__ __forceinline__ void row_step(const LDS double* dXs, const GLB double* rdsrc, bool rd_is_dms, RV* dso) {
     STAMP0();
     for (int r = lanef(); r < ng; r += WAVE) {
       const int k = r / m, i = r - k * m;
@@ -1222,7 +1245,7 @@ struct Solver {
   }
   // restoration step rows: dy, dp, dn, ds (= J dx + c - dp + dn); for the Newton
   // direction also theta_R and the slack/p/n part of grad(phi_R)^T d
-  __device__ __forceinline__ void row_step_resto(const LDS double* dXs, bool soc, GLB double* dso, GLB double* dpo,
+  __device__ __forceinline__ void row_step_resto(const LDS double* dXs, bool soc, RV* dso, GLB double* dpo,
                                                  GLB double* dno, GLB double* dyo, double& th, double& gsum) {
     const double kd = P->o.kappa_d;
     th = 0.0; gsum = 0.0;
@@ -1285,7 +1308,7 @@ struct Solver {
     return pn_of(pn, lg, prox);
   }
   // restoration trial point: theta_R, phi_R and the original objective fo
-  __device__ __forceinline__ bool trial_resto(double a, const GLB double* dUs, const GLB double* dss,
+  __device__ __forceinline__ bool trial_resto(double a, const GLB double* dUs, const RV* dss,
                                               const GLB double* dps, const GLB double* dns, double& fo,
                                               double& phit, double& tht) {
     for (int i = lanef(); i < nw; i += WAVE) Ut[i] = U[i] + a * dUs[i];
@@ -1321,7 +1344,7 @@ struct Solver {
     phit = phb + pn_of(pn, lg, prox);
     return isfinite(phit);
   }
-  __device__ __forceinline__ double frac_to_bound_resto(double tau_, const GLB double* dUs, const GLB double* dss,
+  __device__ __forceinline__ double frac_to_bound_resto(double tau_, const GLB double* dUs, const RV* dss,
                                                         const GLB double* dps, const GLB double* dns) const {
     double b = 1.0;  // p, n bounds in the same pass (min is order-free)
     const double a = frac_to_bound_x(tau_, dUs, dss, [&](int r, bool on) {
@@ -1332,7 +1355,7 @@ struct Solver {
     });
     return fmin(a, wmin(b));
   }
-  __device__ __forceinline__ double dual_frac_to_bound_resto(double tau_, const GLB double* dUs, const GLB double* dss,
+  __device__ __forceinline__ double dual_frac_to_bound_resto(double tau_, const GLB double* dUs, const RV* dss,
                                                              const GLB double* dps, const GLB double* dns) const {
     double b = 1.0;
     const double a = dual_frac_to_bound_x(tau_, dUs, dss, [&](int r, bool on) {
@@ -1347,12 +1370,12 @@ struct Solver {
   }
 
   // primal fraction to the boundary (oracle frac_to_bound)
-  __device__ __forceinline__ double frac_to_bound(double tau_, const GLB double* dUs, const GLB double* dss) const {
+  __device__ __forceinline__ double frac_to_bound(double tau_, const GLB double* dUs, const RV* dss) const {
     return frac_to_bound_x(tau_, dUs, dss, [](int, bool) {});
   }
   // ... with `extra(r, on)` run inside the same pass over the rows
   template <class F>
-  __device__ __forceinline__ double frac_to_bound_x(double tau_, const GLB double* dUs, const GLB double* dss,
+  __device__ __forceinline__ double frac_to_bound_x(double tau_, const GLB double* dUs, const RV* dss,
                                                     F&& extra) const {
     STAMP0();
     double a = 1.0;
@@ -1384,11 +1407,11 @@ struct Solver {
     if (hasl(dl[r])) { const double iS = rcp(s[r] - dl[r]); dvl = mu * iS - vl[r] - vl[r] * iS * dsv; }
     if (hasu(du[r])) { const double iS = rcp(du[r] - s[r]); dvu = mu * iS - vu[r] + vu[r] * iS * dsv; }
   }
-  __device__ __forceinline__ double dual_frac_to_bound(double tau_, const GLB double* dUs, const GLB double* dss) const {
+  __device__ __forceinline__ double dual_frac_to_bound(double tau_, const GLB double* dUs, const RV* dss) const {
     return dual_frac_to_bound_x(tau_, dUs, dss, [](int, bool) {});
   }
   template <class F>
-  __device__ __forceinline__ double dual_frac_to_bound_x(double tau_, const GLB double* dUs, const GLB double* dss,
+  __device__ __forceinline__ double dual_frac_to_bound_x(double tau_, const GLB double* dUs, const RV* dss,
                                                          F&& extra) const {
     STAMP0();
     double a = 1.0;
@@ -1490,7 +1513,7 @@ struct Solver {
 
   // trial point u = U + a dUs, s = s + a dss: rollout into Xt, rows into dt.
   // returns false on an evaluation error (NaN/Inf)
-  __device__ __forceinline__ bool trial(double a, const GLB double* dUs, const GLB double* dss, double& ft, double& phit,
+  __device__ __forceinline__ bool trial(double a, const GLB double* dUs, const RV* dss, double& ft, double& phit,
                         double& tht) {
     for (int i = lanef(); i < nw; i += WAVE) Ut[i] = U[i] + a * dUs[i];
     sync();
@@ -1918,7 +1941,8 @@ __device__ __forceinline__ void resto_phase(const Params* __restrict__ prm, doub
             double th_tr = th, th_old = 0.0, a_soc = a;
             for (int r = S.lanef(); r < ng; r += WAVE) S.cms[r] = S.d[r] - S.s[r] - S.pR[r] + S.nR[r];
             sync();
-            const GLB double *dsp = S.ds, *dpp = S.dpR, *dnp = S.dnR;
+            const auto* dsp = S.ds;
+            const GLB double *dpp = S.dpR, *dnp = S.dnR;
             int cnt = 0;
             bool soc_ok = false;
             while (cnt < o.max_soc && (cnt == 0 || th_tr <= o.kappa_soc * th_old)) {
@@ -1958,7 +1982,7 @@ __device__ __forceinline__ void resto_phase(const Params* __restrict__ prm, doub
         {
           STAMP0();
           const GLB double* dUa = (acc == 2) ? S.dU2 : S.dU;
-          const GLB double* dsa = (acc == 2) ? S.ds2 : S.ds;
+          const auto* dsa = (acc == 2) ? S.ds2 : S.ds;
           const GLB double* dpa = (acc == 2) ? S.dp2R : S.dpR;
           const GLB double* dna = (acc == 2) ? S.dn2R : S.dnR;
           const GLB double* dya = (acc == 2) ? S.dy2R : S.dyR;
@@ -2171,7 +2195,7 @@ __device__ __forceinline__ int solve_one(Solver<CAP>& S, const Params* __restric
     S.rollout(S.U, S.X);
     const double F0 = S.eval_fg(S.X, S.d, nullptr);
     S.derivs(S.X, S.U);
-    S.adjoint(1.0, nullptr);
+    S.adjoint(1.0, (const GLB double*)nullptr);
     double gmax = 0.0;
     bool bad = !isfinite(F0);
     for (int i = S.lanef(); i < nw; i += WAVE) {
@@ -2722,7 +2746,7 @@ __device__ __forceinline__ int solve_one(Solver<CAP>& S, const Params* __restric
             for (int r = S.lanef(); r < ng; r += WAVE) S.dms[r] = S.d[r] - S.s[r];
             int cnt = 0;
             bool soc_acc = false;
-            const GLB double* dsp = S.ds;  // step whose trial is in Ut/dt
+            const auto* dsp = S.ds;  // step whose trial is in Ut/dt
             while (cnt < o.max_soc && (cnt == 0 || th_tr <= o.kappa_soc * th_old)) {
               th_old = th_tr;
               for (int r = S.lanef(); r < ng; r += WAVE) {
@@ -2793,7 +2817,7 @@ __device__ __forceinline__ int solve_one(Solver<CAP>& S, const Params* __restric
     {
       STAMP0();
       const GLB double* dUa = (acc_kind == 2) ? S.dU2 : S.dU;
-      const GLB double* dsa = (acc_kind == 2) ? S.ds2 : S.ds;
+      const auto* dsa = (acc_kind == 2) ? S.ds2 : S.ds;
       S.mu = dir_mu();  // the step's dual components (mu below: the kappa_sigma safeguard)
       if (acc_kind != 3) alpha_d = S.dual_frac_to_bound(tau, dUa, dsa);
       const double ap = alpha_p, ad = alpha_d;
@@ -2919,7 +2943,7 @@ __device__ __forceinline__ int solve_one(Solver<CAP>& S, const Params* __restric
 }
 
 template <class CAP>
-__global__ __launch_bounds__(WAVE, NMPC_WAVES_PER_EU) void nmpc_solve_kernel(const Params* __restrict__ prm, int B, IO io) {
+__global__ __launch_bounds__(WAVE, CAP::wpe) void nmpc_solve_kernel(const Params* __restrict__ prm, int B, IO io) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   const int b = blockIdx.x;
   if (b >= B) return;
@@ -3025,7 +3049,7 @@ __device__ __forceinline__ void cl_step(const Params* __restrict__ prm, int B, c
 
 // K-step closed loop, one workgroup per scenario running its K steps back to back.
 template <class CAP>
-__global__ __launch_bounds__(WAVE, NMPC_WAVES_PER_EU) void nmpc_closed_loop_kernel(const Params* __restrict__ prm, int B, IO io,
+__global__ __launch_bounds__(WAVE, CAP::wpe) void nmpc_closed_loop_kernel(const Params* __restrict__ prm, int B, IO io,
                                                                     Loop lp) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   // workgroups start roughly in blockIdx order, so a caller-supplied permutation sets
@@ -3086,7 +3110,7 @@ __device__ __forceinline__ int xcc_id() {
 }
 
 template <class CAP>
-__global__ __launch_bounds__(WAVE, NMPC_WAVES_PER_EU) void nmpc_closed_loop_sched_kernel(const Params* __restrict__ prm, int B,
+__global__ __launch_bounds__(WAVE, CAP::wpe) void nmpc_closed_loop_sched_kernel(const Params* __restrict__ prm, int B,
                                                                           IO io, Loop lp, SchedQ q) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   const int K = lp.K;
@@ -3249,7 +3273,7 @@ ClassFns nmpc_class_fns_A();
 ClassFns nmpc_class_fns_B();
 ClassFns nmpc_class_fns_C();
 
-using CapA = Cap<20, 15>;   // BASELINE configs 2-4 (N=20, <=10 obstacles) and the reference's N=15 scripts
+using CapA = Cap<20, 15, true>;   // BASELINE configs 2-4 (N=20, <=10 obstacles) and the reference's N=15 scripts
 using CapB = Cap<31, 21>;
 using CapC = Cap<63, 21>;   // any supported shape
 
