@@ -52,25 +52,39 @@ def survey_bytes_per_step(spec, ibar):
     return ibar * b_iter + io, s_stage, b_iter, io
 
 
-def pmc_traffic(kernel, steps, batch):
-    """HBM bytes per launch of `kernel` from the newest committed rocprofv3 PMC
-    summary (profiles/r*_pmc.csv, written by scripts/rocpd_summary.py --csv from
-    the FETCH_SIZE / WRITE_SIZE passes of scripts/profile_round.sh): FETCH_SIZE
-    doubled per the gfx950 correction (MI355X_MICROARCH.md, HBM section),
-    WRITE_SIZE as is, KB -> B.  Only used when the profiled launch had the same
-    steps and batch as this run."""
+def pmc_summary(kernel, steps, batch, warmup):
+    """Counters of `kernel`'s timed launch from the newest committed rocprofv3 PMC
+    summary (profiles/r*_pmc.csv, written by scripts/rocpd_summary.py from the passes
+    of scripts/profile_round.sh), used only when the profiled runs had this run's
+    steps, batch and warm-up.  HBM-side bytes = 2 x FETCH_SIZE + WRITE_SIZE (KB -> B):
+    FETCH_SIZE counts half the bytes of 8 B/lane and 16 B/lane reads alike on gfx950
+    (scripts/fetch_calib.hip, profiles/r02_fetch_calib.csv: 1 GiB read -> 512 MiB
+    counted for both widths; WRITE_SIZE exact for 8 B/lane stores).  Both count
+    L2-to-fabric traffic, Infinity-Cache hits included (MI355X_MICROARCH.md, HBM)."""
     import csv
     import glob
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc.csv")))
     if not files:
-        return None, None
-    vals = {}
+        return None
+    vals, run = {}, {}
     for row in csv.DictReader(open(files[-1])):
-        if kernel in row["kernel"] and row.get("steps", "") == str(steps) and row.get("batch", "") == str(batch):
+        if (kernel in row["kernel"] and row.get("steps", "") == str(steps) and row.get("batch", "") == str(batch)
+                and row.get("warmup", "") == str(warmup)):
             vals[row["counter"]] = float(row["value"])
+            run.setdefault(row["counter"], {k: row.get(k) for k in ("ibar", "kernel_ms", "bench_value")})
     if "FETCH_SIZE" not in vals or "WRITE_SIZE" not in vals:
-        return None, None
-    return (2.0 * vals["FETCH_SIZE"] + vals["WRITE_SIZE"]) * 1024.0, os.path.relpath(files[-1], ROOT)
+        return None
+    out = {"traffic": (2.0 * vals["FETCH_SIZE"] + vals["WRITE_SIZE"]) * 1024.0,
+           "source": os.path.relpath(files[-1], ROOT), "profiled_runs": run}
+    if vals.get("SQ_WAVE_CYCLES"):
+        wc = vals["SQ_WAVE_CYCLES"]
+        out["sq"] = {"wait_any_frac": vals.get("SQ_WAIT_ANY", 0) / wc,
+                     "valu_active_frac": vals.get("SQ_ACTIVE_INST_VALU", 0) / wc,
+                     "lds_active_frac": vals.get("SQ_ACTIVE_INST_LDS", 0) / wc,
+                     "wait_inst_frac": vals.get("SQ_WAIT_INST_ANY", 0) / wc}
+    if vals.get("TCC_HIT_sum") is not None and vals.get("TCC_MISS_sum") is not None:
+        out["l2_hit_rate"] = vals["TCC_HIT_sum"] / max(1.0, vals["TCC_HIT_sum"] + vals["TCC_MISS_sum"])
+    return out
 
 
 def _cpu_worker(args):
@@ -90,20 +104,21 @@ def _cpu_worker(args):
     solver = orc.IpoptDense(prob, orc.REFERENCE_OPTS)
     nx, nu = prob.nx, prob.nu
     t0 = time.perf_counter()
-    times, iters, stats = [], [], []
+    times, iters, stats, recs = [], [], [], []
     for row in range(i, P.shape[0], nproc):
         x0, xs, u0 = P[row, :nx].copy(), P[row, nx:nx + 3].copy(), np.zeros(len(lbx))
-        for _ in range(K):
+        for k in range(K):
             if time.perf_counter() - t0 >= budget_s:
-                return times, iters, stats
+                return times, iters, stats, recs
             t1 = time.perf_counter()
             r = solver.solve(u0, lbx, ubx, lbg, ubg, np.concatenate([x0, xs, P[row, nx + 3:]]))
             times.append(time.perf_counter() - t1)
             iters.append(r["iter"])
             stats.append(r["status"])
+            recs.append((row, k, r["status"], r["x"][:nu].copy(), r["f"]))
             x0, u1, xs = orc.shift_timestep(prob, x0, r["x"].reshape(N, nu).T, xs, con_t=(12.0, 0.01))
             u0 = u1.T.ravel()
-    return times, iters, stats
+    return times, iters, stats, recs
 
 
 def cpu_baseline(spec_cfg, cfg, P, lbx, ubx, lbg, ubg, K, budget_s=15.0):
@@ -130,6 +145,8 @@ def cpu_baseline(spec_cfg, cfg, P, lbx, ubx, lbg, ubg, K, budget_s=15.0):
     iters = np.concatenate([np.asarray(r[1], dtype=float) for r in res])
     sts = np.concatenate([np.asarray(r[2], dtype=int) for r in res])
     n = len(times)
+    cpu_baseline.records = [rec for r in res for rec in r[3]]
+    cpu_baseline.sample_rows = sample.shape[0]
     return {"value": n / wall, "unit": "MPC steps/s", "cores": nproc, "kind": "port",
             "sample": f"{n} warm-started closed-loop MPC steps (solve + shift, up to {K} per scenario) of "
                       f"config-{cfg} scenarios by oracle/nmpc_oracle.py (numpy dense single-shooting IPOPT "
@@ -140,11 +157,61 @@ def cpu_baseline(spec_cfg, cfg, P, lbx, ubx, lbg, ubg, K, budget_s=15.0):
             "status_histogram": {int(k): int(v) for k, v in zip(*np.unique(sts, return_counts=True))}}
 
 
+def parity_sample(solver, spec, P, K, records, bnd, dev, tol=1e-6):
+    """GPU vs the CPU leg on the same (scenario, step) pairs: the CPU leg's scenarios
+    rerun through nmpc_closed_loop_dev from the same start (w = 0, the same p and
+    target controls), compared step by step until a chain first disagrees -- status,
+    and for converged steps u0 and f within tol (1 + |ref|) (the north-star 1e-6)."""
+    import torch
+
+    rows = sorted({r[0] for r in records})
+    if not rows:
+        return None
+    idx = {r: j for j, r in enumerate(rows)}
+    B = len(rows)
+    f64 = dict(dtype=torch.float64, device=dev)
+    hist = {"u": torch.empty(K, B, 6, **f64), "f": torch.empty(K, B, **f64),
+            "status": torch.empty(K, B, dtype=torch.int32, device=dev)}
+    solver.closed_loop_device(K, *bnd, torch.tensor(P[rows], **f64).contiguous(), torch.zeros(B, spec.nw, **f64),
+                              torch.full((B,), 12.0, **f64), torch.full((B,), 0.01, **f64), hist)
+    H = {k: v.cpu().numpy() for k, v in hist.items()}
+    by = {}
+    for row, k, st, u0, f in records:
+        by.setdefault(row, []).append((k, st, u0, f))
+    compared = agree_status = before_div = chains_same = 0
+    max_u, max_f = 0.0, 0.0
+    for row, steps in by.items():
+        j, same = idx[row], True
+        for k, st, u0, f in sorted(steps, key=lambda t: t[0]):
+            compared += 1
+            gs = int(H["status"][k, j])
+            agree_status += gs == st
+            if not same:
+                continue
+            ok = gs == st
+            if ok and st in (0, 1):
+                eu = float(np.max(np.abs(H["u"][k, j, :len(u0)] - u0) / (1 + np.abs(u0))))
+                ef = abs(float(H["f"][k, j]) - f) / (1 + abs(f))
+                ok = eu <= tol and ef <= tol
+                if ok:
+                    max_u, max_f = max(max_u, eu), max(max_f, ef)
+            if ok:
+                before_div += 1
+            else:
+                same = False
+        chains_same += same
+    return {"scenarios": len(by), "steps_compared": compared,
+            "status_agreement": agree_status / max(1, compared),
+            "steps_before_first_divergence": before_div, "chains_identical": chains_same,
+            "max_u0_relerr": max_u, "max_f_relerr": max_f, "tol": tol,
+            "reference": "oracle/nmpc_oracle.py (the cpu_baseline leg's own solves)"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20, help="closed-loop MPC steps per scenario (timed)")
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=4096, help="scenarios per GPU")
     ap.add_argument("--config", type=int, default=3)
     ap.add_argument("--mode", choices=["fused", "per_step", "cold"], default="fused",
@@ -281,6 +348,7 @@ def main():
         sts = ht["status"].cpu().numpy()
         hist = {int(s_): int((sts == s_).sum()) for s_ in np.unique(sts)}
         timed_run.fov = float(ht["fov"].mean().item())
+        timed_run.chain = ht["iters"].sum(0).cpu().numpy()
         return float(el_t.item()), kern_ms, float(tot[0].item() / tot[1].item()), hist
 
     elapsed, kern_ms, ibar, status_hist = timed_run(args.mode, p0.clone(), w0.clone())
@@ -307,7 +375,8 @@ def main():
         achieved_tf = flops_launch / kern_avg_s / 1e12
         bps, s_stage, b_iter, io = survey_bytes_per_step(spec, ibar)
         achieved_gbs = B * steps_per_launch * bps / kern_avg_s / 1e9
-        traffic, traffic_src = pmc_traffic(kname, K if args.mode == "fused" else None, B)
+        pmc = pmc_summary(kname, K if args.mode == "fused" else None, B, W)
+        traffic = pmc["traffic"] if pmc else None
         mode_txt = {"fused": f"{K} warm-started closed-loop MPC steps per scenario in one launch",
                     "per_step": "warm-started closed-loop MPC steps, one launch per step",
                     "cold": "cold-start (u=0) solves, one launch per step"}[args.mode]
@@ -324,8 +393,14 @@ def main():
                        "global_batch": B * world, "seq_len": spec.N, "parallelism": f"dp{world}"},
             "roofline": {"bound": "hbm", "achieved": achieved_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved_gbs / HBM_PEAK_GBS, "traffic": traffic,
-                         "traffic_unit": "HBM bytes per launch (2*FETCH_SIZE + WRITE_SIZE, rocprofv3 PMC)",
-                         "traffic_source": traffic_src,
+                         "traffic_unit": "bytes per launch between L2 and the fabric (Infinity Cache or HBM): "
+                                         "2*FETCH_SIZE + WRITE_SIZE, rocprofv3 PMC (calibrated x2 for 8 and 16 B/lane "
+                                         "reads, scripts/fetch_calib.hip)",
+                         "traffic_source": pmc["source"] if pmc else None,
+                         "counter_bytes_frac": (traffic / kern_avg_s / 1e9 / HBM_PEAK_GBS) if traffic else None,
+                         "pmc_runs": pmc["profiled_runs"] if pmc else None,
+                         "sq": pmc.get("sq") if pmc else None,
+                         "l2_hit_rate": pmc.get("l2_hit_rate") if pmc else None,
                          "kernel": kname, "kernel_avg_ms": kern_avg_s * 1e3, "launches": n_launch,
                          "model": f"SURVEY 8(d) streamed-KKT bytes: I_bar x B_iter + IO = {bps:.0f} B per "
                                   f"MPC step (I_bar={ibar:.2f}, B_iter={b_iter} B, IO={io} B) x B={B} x "
@@ -337,6 +412,17 @@ def main():
             "mean_ip_iterations": ibar,
             "status_histogram": status_hist,
         }
+        if args.mode == "fused":
+            # the launch is bounded by its longest scenario chain (K steps of up to max_iter
+            # iterations each) and by the total work over the persistent slots
+            ch = timed_run.chain
+            slots = timed_run.info["launched_waves"] if timed_run.info["policy"] == "step_queues" else B
+            res["roofline"]["chain"] = {
+                "max_chain_iterations": int(ch.max()), "mean_chain_iterations": float(ch.mean()),
+                "total_iterations": int(ch.sum()), "slots": int(min(slots, B)),
+                "ms_per_chain_iteration": kern_avg_s * 1e3 / float(ch.max()),
+                "work_bound_iterations_per_slot": float(ch.sum()) / min(slots, B),
+                "note": "launch >= max(max_chain, total/slots) x per-iteration time"}
         if args.mode == "fused":
             info = timed_run.info
             first = ("index order" if (args.in_order or W == 0) else
@@ -356,6 +442,9 @@ def main():
             res["per_step_launch"] = side
         if cpu_res is not None:
             res["cpu_baseline"] = cpu_res
+            if world == 1 and getattr(cpu_baseline, "records", None):
+                res["parity_sample"] = parity_sample(solver, spec, P_all[:cpu_baseline.sample_rows], K,
+                                                     cpu_baseline.records, bnd, dev)
         print(json.dumps(res))
     if world > 1:
         dist.destroy_process_group()

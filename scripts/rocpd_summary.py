@@ -1,19 +1,38 @@
-"""Summarise rocprofv3 rocpd databases: kernel durations, and PMC counters of
-the LAST dispatch of each kernel (the bench's timed launch).
-usage: python scripts/rocpd_summary.py [--csv out.csv --steps K --batch B] <dir> [...]"""
-import argparse, csv, glob, os, sqlite3
+"""Summarise rocprofv3 rocpd databases: kernel durations, and PMC counters of the
+timed dispatch of each kernel (the LAST dispatch: bench.py launches the fused kernel
+twice, a scratch-copy launch and then the timed one).  Each pass directory's sibling
+log (<dir>.log) holds that pass's bench JSON line; its steps / warmup / batch / mean
+IP iterations / HIP-event kernel time are written next to every counter row.
+usage: python scripts/rocpd_summary.py [--csv out.csv] <pass dir> [...]"""
+import argparse, csv, glob, json, os, sqlite3
 
 ap = argparse.ArgumentParser()
 ap.add_argument("dirs", nargs="+")
 ap.add_argument("--csv")
-ap.add_argument("--steps", default="")
-ap.add_argument("--batch", default="")
 a = ap.parse_args()
+
+
+def bench_line(d):
+    log = d.rstrip("/") + ".log"
+    if not os.path.exists(log):
+        return {}
+    for line in reversed(open(log).read().splitlines()):
+        if line.startswith("{") and '"metric"' in line:
+            return json.loads(line)
+    return {}
+
+
 rows = []
 for d in a.dirs:
+    bl = bench_line(d)
+    run = {"steps": bl.get("steps", ""), "warmup": bl.get("warmup", ""),
+           "batch": bl.get("config", {}).get("global_batch", ""),
+           "ibar": bl.get("mean_ip_iterations", ""),
+           "kernel_ms": bl.get("roofline", {}).get("kernel_avg_ms", ""),
+           "bench_value": bl.get("value", "")}
     for f in glob.glob(os.path.join(d, "**", "*.db"), recursive=True):
         db = sqlite3.connect(f)
-        print(f"== {f}")
+        print(f"== {f}  run: {run}")
         n = db.execute("select count(*) from counters_collection").fetchone()[0]
         if n:
             q = ("select kernel_name, counter_name, value, dispatch_id from counters_collection c "
@@ -22,8 +41,7 @@ for d in a.dirs:
             for kn, cn, v, did in db.execute(q):
                 if "nmpc" in kn:
                     print(f"  {kn[:60]:60s} {cn:24s} dispatch={did} value={v:.6g}")
-                    rows.append({"kernel": kn, "counter": cn, "value": v, "dispatch": did,
-                                 "steps": a.steps, "batch": a.batch})
+                    rows.append({"kernel": kn, "counter": cn, "value": v, "dispatch": did, **run})
         else:
             q = ("select name, count(*), avg(duration), min(duration), max(duration), sum(duration) "
                  "from kernels group by name order by sum(duration) desc")
