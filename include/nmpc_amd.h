@@ -75,6 +75,10 @@ typedef struct nmpc_options {
   /* watchdog procedure of the backtracking line search (IPOPT defaults 10 and 3;
    * a trigger of 0 disables it) */
   int32_t watchdog_shortened_iter_trigger, watchdog_trial_iter_max;
+  /* not an IPOPT option: 1 = Riccati factorisation and solves in fp32 (the fp32 leg of
+   * BASELINE config 5's fp32-vs-fp64 sweep); the iterate, residuals, line search and
+   * termination tests stay fp64.  0 (default) = fp64 throughout. */
+  int32_t linear_solver_fp32, reserved0;
   double tol, acceptable_tol, acceptable_obj_change_tol, acceptable_dual_inf_tol;
   double acceptable_constr_viol_tol, acceptable_compl_inf_tol;
   double dual_inf_tol, constr_viol_tol, compl_inf_tol;

@@ -70,7 +70,7 @@ struct Params {
 // register plus an immediate: no pointer registers in the kernel.
 struct Lay {
   // global workspace (64 B aligned slices)
-  int U, Ut, dU, dU2, zl, zu, xl, xu, sigx, ru;
+  int U, Ut, dU, dU2, zl, zu, xl, xu, sigx, ru, rres, dUr;
   int s, y, vl, vu, d, dt, ds, ds2, dc, dl, du, dms, filt;
   int gl, Hl, Qs, K, Rk;        // stage data / Riccati factors (global copies)
   // restoration phase: reference/backup iterate, p/n and their multipliers, steps, filter
@@ -83,7 +83,7 @@ struct Lay {
   int X, Xt, dX;
   int trig, qs, lam;
   int kf, Rc, P0, P1, pv0, pv1, St;
-  int p, ob, inc, red, rvars;
+  int p, ob, inc, red, rvars, rdX;
   int total;    // LDS doubles per scenario
   int wstotal;  // global-workspace doubles per scenario
 };
@@ -92,13 +92,14 @@ constexpr int al8(int n) { return (n + 7) & ~7; }
 // lr: the main iteration's hot row vectors (s, y, vl, vu, d, ds, ds2, dc) live in LDS
 // (capacity classes with a small row count: the row passes then never wait on L2 /
 // Infinity-Cache latency); otherwise in the global workspace
-constexpr Lay make_layout(int N, int m, bool lr) {
+constexpr Lay make_layout(int N, int m, bool lr, bool refine) {
   Lay L{};
   const int nw = 6 * N, ng = m * (N + 1), nX = 8 * (N + 1), NS = N + 1;
   int g = 0, o = 0;
   L.U = g; g += al8(nw); L.Ut = g; g += al8(nw); L.dU = g; g += al8(nw); L.dU2 = g; g += al8(nw);
   L.zl = g; g += al8(nw); L.zu = g; g += al8(nw); L.xl = g; g += al8(nw); L.xu = g; g += al8(nw);
   L.sigx = g; g += al8(nw); L.ru = g; g += al8(nw);
+  L.rres = g; g += al8(nw); L.dUr = g; g += al8(nw);  // iterative refinement (fp32 classes)
   if (!lr) {
     L.s = g; g += al8(ng); L.y = g; g += al8(ng); L.vl = g; g += al8(ng); L.vu = g; g += al8(ng);
     L.d = g; g += al8(ng); L.ds = g; g += al8(ng); L.ds2 = g; g += al8(ng); L.dc = g; g += al8(ng);
@@ -126,6 +127,7 @@ constexpr Lay make_layout(int N, int m, bool lr) {
   L.p = o; o += 64; L.ob = o; o += al2(2 * NMPC_MAX_OBS); L.inc = o; o += al2(8 * NS); L.red = o; o += 24;
   L.dl = o; o += al2(ng); L.du = o; o += al2(ng);  // row bounds (constant during a solve, read by every row pass)
   L.rvars = o; o += 48;  // line-search / restoration scalars; [32..36] barrier sums; [40..45] watchdog
+  L.rdX = o; if (refine) o += al2(nX);  // refinement step in X (fp32 classes)
   if (lr) {
     L.s = o; o += al2(ng); L.y = o; o += al2(ng); L.vl = o; o += al2(ng); L.vu = o; o += al2(ng);
     L.d = o; o += al2(ng); L.ds = o; o += al2(ng); L.ds2 = o; o += al2(ng); L.dc = o; o += al2(ng);
@@ -140,13 +142,18 @@ constexpr Lay make_layout(int N, int m, bool lr) {
 
 // LDSR: hot row vectors in LDS (make_layout); such a class needs ~39 KB of LDS per
 // scenario, so it runs one wave per SIMD (four per CU) with the full 512-VGPR budget
-template <int NMAX, int MMAX, bool LDSR = false>
+// RT: arithmetic type of the Riccati factorisation and its solves (double: the
+// reference's fp64; float: the fp32 leg of BASELINE config 5's fp32-vs-fp64 sweep --
+// everything else, the iterate, residuals, line search and termination tests, stays fp64)
+template <int NMAX, int MMAX, bool LDSR = false, class RTYPE = double>
 struct Cap {
   static constexpr int nmax = NMAX, mmax = MMAX;
   static constexpr bool lds_rows = LDSR;
+  using RT = RTYPE;
   static constexpr int wpe = LDSR ? 1 : NMPC_WAVES_PER_EU;
   using RowT = std::conditional_t<LDSR, LDS double, GLB double>;
-  static constexpr Lay L = make_layout(NMAX, MMAX, LDSR);
+  static constexpr bool refine = !std::is_same<RTYPE, double>::value;  // fp64 refinement of fp32 solves
+  static constexpr Lay L = make_layout(NMAX, MMAX, LDSR, refine);
   // row passes: trips of 64 rows processed together (their loads batched), <= 5
   static constexpr int rtrips = (MMAX * (NMAX + 1) + 63) / 64;
   static constexpr int ru = rtrips < 2 ? rtrips : 2;
@@ -226,6 +233,10 @@ __device__ __forceinline__ double rsq(double x) {
   y = fma(y, r, y);
   r = fma(-h * y, y, 0.5);
   return fma(y, r, y);
+}
+__device__ __forceinline__ float rsq(float x) { return __builtin_amdgcn_rsqf(x); }  // v_rsq_f32, ~1 ulp
+__device__ __forceinline__ float readlane_d(float v, int l) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
 }
 // Cross-lane hand-off inside the (single-wave) workgroup.  Every kernel here runs
 // exactly one wavefront per workgroup, so a wavefront-scope fence is the complete
@@ -318,7 +329,8 @@ struct Solver {
   int nb, nuE, nwE;  // box rows per stage; real controls per stage; real decision length
   double T;
   // pointers into LDS
-  GLB double* U, *Ut, *dU, *dU2, *zl, *zu, *xl, *xu, *sigx, *ru;
+  GLB double* U, *Ut, *dU, *dU2, *zl, *zu, *xl, *xu, *sigx, *ru, *rres, *dUr;
+  LDS double* rdX;
   LDS double* X, *Xt, *dX;
   using RV = typename CAP::RowT;  // hot row vectors: LDS or global (Cap::lds_rows)
   RV *s, *y, *vl, *vu, *d, *ds, *ds2, *dc;
@@ -349,7 +361,7 @@ struct Solver {
     GLB double* gw = (GLB double*)(wsp + (long long)b_ * L.wstotal);
     U = gw + L.U; Ut = gw + L.Ut; dU = gw + L.dU; dU2 = gw + L.dU2;
     zl = gw + L.zl; zu = gw + L.zu; xl = gw + L.xl; xu = gw + L.xu;
-    sigx = gw + L.sigx; ru = gw + L.ru;
+    sigx = gw + L.sigx; ru = gw + L.ru; rres = gw + L.rres; dUr = gw + L.dUr; rdX = sm + L.rdX;
     X = sm + L.X; Xt = sm + L.Xt; dX = sm + L.dX;
     auto rvp = [&](int off) -> RV* {
       if constexpr (CAP::lds_rows) return (RV*)(sm + off);
@@ -876,17 +888,22 @@ struct Solver {
     STAMP1(PH_RIC);
     return r;
   }
+  // arithmetic in CAP::RT (the LDS exchange arrays hold RT values)
   __device__ __forceinline__ bool riccati_(const GLB double* Rd, const GLB double* rv) {
+    using R = typename CAP::RT;
     // one opaque lane index for the whole sweep (every lanef() call is a fresh register copy)
     const int ln = lanef();
     const int i = ln >> 3, j = ln & 7;
     const int ij = (i <= j) ? pk8(i, j) : pk8(j, i);
-    LDS double* Pc = Pa;
-    LDS double* Pn = Pb;
-    LDS double* pc = pva;
-    LDS double* pn = pvb;
-    Pc[ln] = Qs[N * 36 + ij];
-    if (ln < 8) pc[ln] = qs[N * 10 + ln];
+    LDS R* Pc = (LDS R*)Pa;
+    LDS R* Pn = (LDS R*)Pb;
+    LDS R* pc = (LDS R*)pva;
+    LDS R* pn = (LDS R*)pvb;
+    LDS R* Stc = (LDS R*)St;
+    LDS R* Rcc = (LDS R*)Rc;
+    const R Tr = (R)T, dlt = (R)delta;
+    Pc[ln] = (R)Qs[N * 36 + ij];
+    if (ln < 8) pc[ln] = (R)qs[N * 10 + ln];
     // lanes 48..63 -> R~ entries t = 0..15, lanes 0..4 -> t = 16..20 (packed lower)
     const int tR = ln >= 48 ? ln - 48 : (ln < 5 ? 16 + ln : -1);
     int rR = 0;
@@ -908,72 +925,75 @@ struct Solver {
     sync();
     bool ok = true;
     for (int k = N - 1; k >= 0; --k) {
-      const double qv = qvn, rdk = rdn, rvk = rvn;
+      const R qv = (R)qvn, rdk = (R)rdn, rvk = (R)rvn;
       if (k > 0) {
         qvn = Qs[(k - 1) * 36 + ij];
         if (diagR && Rd) rdn = Rd[(k - 1) * 6 + rR];
         rvn = rv[(k - 1) * 6 + lr];
       }
-      double E03, E04, E13, E14, E23, b00, b10, b20;
-      stage_AB(k, E03, E04, E13, E14, E23, b00, b10, b20);
-      const double aj0 = (j == 3) ? E03 : (j == 4 ? E04 : 0.0);
-      const double aj1 = (j == 3) ? E13 : (j == 4 ? E14 : 0.0);
-      const double aj2 = (j == 3) ? E23 : 0.0;
-      const double ai0 = (i == 3) ? E03 : (i == 4 ? E04 : 0.0);
-      const double ai1 = (i == 3) ? E13 : (i == 4 ? E14 : 0.0);
-      const double ai2 = (i == 3) ? E23 : 0.0;
-      double APA;
+      double E03d, E04d, E13d, E14d, E23d, b00d, b10d, b20d;
+      stage_AB(k, E03d, E04d, E13d, E14d, E23d, b00d, b10d, b20d);
+      const R E03 = (R)E03d, E04 = (R)E04d, E13 = (R)E13d, E14 = (R)E14d, E23 = (R)E23d;
+      const R b00 = (R)b00d, b10 = (R)b10d, b20 = (R)b20d;
+      const R zr = (R)0;
+      const R aj0 = (j == 3) ? E03 : (j == 4 ? E04 : zr);
+      const R aj1 = (j == 3) ? E13 : (j == 4 ? E14 : zr);
+      const R aj2 = (j == 3) ? E23 : zr;
+      const R ai0 = (i == 3) ? E03 : (i == 4 ? E04 : zr);
+      const R ai1 = (i == 3) ? E13 : (i == 4 ? E14 : zr);
+      const R ai2 = (i == 3) ? E23 : zr;
+      R APA;
       // ---- (1)
       { STAMP0();
-        const double P00 = Pc[0], P01 = Pc[1], P02 = Pc[2], P11 = Pc[9], P12 = Pc[10], P22 = Pc[18];
-        const double P0j = Pc[j], P1j = Pc[8 + j], P2j = Pc[16 + j];
-        const double Pi0 = Pc[i * 8], Pi1 = Pc[i * 8 + 1], Pi2 = Pc[i * 8 + 2], Pij = Pc[ln];
-        const double PA0j = P0j + ((P00 * aj0 + P01 * aj1) + P02 * aj2);
-        const double PA1j = P1j + ((P01 * aj0 + P11 * aj1) + P12 * aj2);
-        const double PA2j = P2j + ((P02 * aj0 + P12 * aj1) + P22 * aj2);
-        const double PAij = Pij + ((Pi0 * aj0 + Pi1 * aj1) + Pi2 * aj2);
+        const R P00 = Pc[0], P01 = Pc[1], P02 = Pc[2], P11 = Pc[9], P12 = Pc[10], P22 = Pc[18];
+        const R P0j = Pc[j], P1j = Pc[8 + j], P2j = Pc[16 + j];
+        const R Pi0 = Pc[i * 8], Pi1 = Pc[i * 8 + 1], Pi2 = Pc[i * 8 + 2], Pij = Pc[ln];
+        const R PA0j = P0j + ((P00 * aj0 + P01 * aj1) + P02 * aj2);
+        const R PA1j = P1j + ((P01 * aj0 + P11 * aj1) + P12 * aj2);
+        const R PA2j = P2j + ((P02 * aj0 + P12 * aj1) + P22 * aj2);
+        const R PAij = Pij + ((Pi0 * aj0 + Pi1 * aj1) + Pi2 * aj2);
         APA = PAij + ((ai0 * PA0j + ai1 * PA1j) + ai2 * PA2j);
-        const double Prj = Pc[rowS * 8 + j], Pr0 = Pc[rowS * 8], Pr1 = Pc[rowS * 8 + 1], Pr2 = Pc[rowS * 8 + 2];
-        const double PArj = Prj + ((Pr0 * aj0 + Pr1 * aj1) + Pr2 * aj2);
-        double stv = (i == 0) ? ((b00 * PA0j + b10 * PA1j) + b20 * PA2j) : T * PArj;
-        stv += (i == 0 && j == 3) ? qs[k * 10 + 8] : ((i == 0 && j == 4) ? qs[k * 10 + 9] : 0.0);
-        if (ln < 48) St[ln] = stv;
+        const R Prj = Pc[rowS * 8 + j], Pr0 = Pc[rowS * 8], Pr1 = Pc[rowS * 8 + 1], Pr2 = Pc[rowS * 8 + 2];
+        const R PArj = Prj + ((Pr0 * aj0 + Pr1 * aj1) + Pr2 * aj2);
+        R stv = (i == 0) ? ((b00 * PA0j + b10 * PA1j) + b20 * PA2j) : Tr * PArj;
+        stv += (i == 0 && j == 3) ? (R)qs[k * 10 + 8] : ((i == 0 && j == 4) ? (R)qs[k * 10 + 9] : zr);
+        if (ln < 48) Stc[ln] = stv;
         if (tR >= 0) {
-          double v;
+          R v;
           if (rR == 0) {  // b0^T P[0:3,0:3] b0
             v = b00 * ((P00 * b00 + P01 * b10) + P02 * b20) + b10 * ((P01 * b00 + P11 * b10) + P12 * b20) +
                 b20 * ((P02 * b00 + P12 * b10) + P22 * b20);
           } else if (cR == 0) {
-            const LDS double* Pr = Pc + (2 + rR) * 8;
-            v = T * ((Pr[0] * b00 + Pr[1] * b10) + Pr[2] * b20);
+            const LDS R* Pr = Pc + (2 + rR) * 8;
+            v = Tr * ((Pr[0] * b00 + Pr[1] * b10) + Pr[2] * b20);
           } else {
-            v = T * (T * Pc[(2 + rR) * 8 + 2 + cR]);
+            v = Tr * (Tr * Pc[(2 + rR) * 8 + 2 + cR]);
           }
           // an absent control (model embedding) keeps a unit pivot: zero step, no inertia effect
-          if (rR == cR) v = (rR >= nuE) ? 1.0 : v + (rdk + delta);
-          Rc[tR] = v;
-          Rk[k * 21 + tR] = v;
+          if (rR == cR) v = (rR >= nuE) ? (R)1 : v + (rdk + dlt);
+          Rcc[tR] = v;
+          Rk[k * 21 + tR] = (double)v;
         }
         sync();
         STAMP1(PH_RA); }
       // ---- (2)
-      double rt[6];
+      R rt[6];
       { STAMP0();
-        double Lm[21], idg[6];
+        R Lm[21], idg[6];
 #pragma unroll
-        for (int t = 0; t < 21; ++t) Lm[t] = Rc[t];
+        for (int t = 0; t < 21; ++t) Lm[t] = Rcc[t];
 #pragma unroll
         for (int c = 0; c < 6; ++c) {
-          double dg = Lm[c * (c + 1) / 2 + c];
+          R dg = Lm[c * (c + 1) / 2 + c];
 #pragma unroll
           for (int t = 0; t < c; ++t) dg -= Lm[c * (c + 1) / 2 + t] * Lm[c * (c + 1) / 2 + t];
-          if (!(dg > 0.0)) ok = false;
-          const double ig = rsq(dg);
+          if (!(dg > zr)) ok = false;
+          const R ig = rsq(dg);
           Lm[c * (c + 1) / 2 + c] = dg * ig;
           idg[c] = ig;
 #pragma unroll
           for (int r = c + 1; r < 6; ++r) {
-            double v = Lm[r * (r + 1) / 2 + c];
+            R v = Lm[r * (r + 1) / 2 + c];
 #pragma unroll
             for (int t = 0; t < c; ++t) v -= Lm[r * (r + 1) / 2 + t] * Lm[c * (c + 1) / 2 + t];
             Lm[r * (r + 1) / 2 + c] = v * ig;
@@ -981,12 +1001,12 @@ struct Solver {
         }
         rt[0] = readlane_d(rvk, 0) + ((b00 * pc[0] + b10 * pc[1]) + b20 * pc[2]);
 #pragma unroll
-        for (int r = 1; r < 6; ++r) rt[r] = readlane_d(rvk, r) + T * pc[2 + r];
-        double ya[6], yb[6];
+        for (int r = 1; r < 6; ++r) rt[r] = readlane_d(rvk, r) + Tr * pc[2 + r];
+        R ya[6], yb[6];
 #pragma unroll
         for (int r = 0; r < 6; ++r) {
-          double a = St[r * 8 + i];
-          double bb = (ln == 8) ? rt[r] : St[r * 8 + j];
+          R a = Stc[r * 8 + i];
+          R bb = (ln == 8) ? rt[r] : Stc[r * 8 + j];
 #pragma unroll
           for (int t = 0; t < r; ++t) {
             a -= Lm[r * (r + 1) / 2 + t] * ya[t];
@@ -996,115 +1016,197 @@ struct Solver {
           yb[r] = bb * idg[r];
         }
         if (upper) {
-          double sy = 0.0;
+          R sy = zr;
 #pragma unroll
           for (int r = 0; r < 6; ++r) sy += ya[r] * yb[r];
-          const double pv = (qv + APA) - sy;
+          const R pv = (qv + APA) - sy;
           Pn[ln] = pv;
           Pn[ji] = pv;
         }
         if (ln < 9) {
 #pragma unroll
           for (int r = 5; r >= 0; --r) {
-            double a = yb[r];
+            R a = yb[r];
 #pragma unroll
             for (int t = r + 1; t < 6; ++t) a -= Lm[t * (t + 1) / 2 + r] * yb[t];
             yb[r] = a * idg[r];
           }
           if (ln < 8) {
 #pragma unroll
-            for (int r = 0; r < 6; ++r) K[k * 48 + r * 8 + ln] = -yb[r];
-            double atp = pc[ln];
+            for (int r = 0; r < 6; ++r) K[k * 48 + r * 8 + ln] = (double)(-yb[r]);
+            R atp = pc[ln];
             if (ln == 3) atp = atp + ((E03 * pc[0] + E13 * pc[1]) + E23 * pc[2]);
             else if (ln == 4) atp = atp + (E04 * pc[0] + E14 * pc[1]);
-            double kr = 0.0;
+            R kr = zr;
 #pragma unroll
             for (int r = 0; r < 6; ++r) kr += (-yb[r]) * rt[r];
-            pn[ln] = (qs[k * 10 + ln] + atp) + kr;
+            pn[ln] = ((R)qs[k * 10 + ln] + atp) + kr;
           } else {
 #pragma unroll
-            for (int r = 0; r < 6; ++r) kf[k * 6 + r] = -yb[r];
+            for (int r = 0; r < 6; ++r) kf[k * 6 + r] = (double)(-yb[r]);
           }
         }
         sync();
         STAMP1(PH_RD); }
       ok = !wany(!ok);  // every lane computed the same pivots; make it explicit
       if (!ok) break;
-      LDS double* t1 = Pc; Pc = Pn; Pn = t1;
-      LDS double* t2 = pc; pc = pn; pn = t2;
+      LDS R* t1 = Pc; Pc = Pn; Pn = t1;
+      LDS R* t2 = pc; pc = pn; pn = t2;
     }
     return ok;
   }
 
   // gradient-only re-solve with the stored factors (second-order correction):
   // every lanef() runs the vector recursion redundantly (R~_k re-factorised).
+  // ZQ: linear state terms q_k = 0 (the refinement's right-hand side is a control residual)
+  template <bool ZQ = false>
   __device__ __forceinline__ void resolve(const GLB double* rv) {
 #ifdef NMPC_STAMPS
     if (lanef() == 0) stamps[PH_RC] += 1.0;  // count SOC re-solves
 #endif
     STAMP0();
-    double p8[8];
+    using R = typename CAP::RT;  // the factorisation's precision
+    R p8[8];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) p8[i] = qs[N * 10 + i];
+    for (int i = 0; i < 8; ++i) p8[i] = ZQ ? (R)0 : (R)qs[N * 10 + i];
     for (int k = N - 1; k >= 0; --k) {
-      double E03, E04, E13, E14, E23, b00, b10, b20;
-      stage_AB(k, E03, E04, E13, E14, E23, b00, b10, b20);
-      double Lm[21], idg[6], rt[6], v[6];
+      double E03d, E04d, E13d, E14d, E23d, b00d, b10d, b20d;
+      stage_AB(k, E03d, E04d, E13d, E14d, E23d, b00d, b10d, b20d);
+      const R E03 = (R)E03d, E04 = (R)E04d, E13 = (R)E13d, E14 = (R)E14d, E23 = (R)E23d;
+      const R b00 = (R)b00d, b10 = (R)b10d, b20 = (R)b20d, Tr = (R)T;
+      R Lm[21], idg[6], rt[6], v[6];
 #pragma unroll
-      for (int t = 0; t < 21; ++t) Lm[t] = Rk[k * 21 + t];
+      for (int t = 0; t < 21; ++t) Lm[t] = (R)Rk[k * 21 + t];
 #pragma unroll
       for (int c = 0; c < 6; ++c) {
-        double dg = Lm[c * (c + 1) / 2 + c];
+        R dg = Lm[c * (c + 1) / 2 + c];
 #pragma unroll
         for (int t = 0; t < c; ++t) dg -= Lm[c * (c + 1) / 2 + t] * Lm[c * (c + 1) / 2 + t];
-        const double ig = rsq(dg);
+        const R ig = rsq(dg);
         Lm[c * (c + 1) / 2 + c] = dg * ig;
         idg[c] = ig;
 #pragma unroll
         for (int r = c + 1; r < 6; ++r) {
-          double a = Lm[r * (r + 1) / 2 + c];
+          R a = Lm[r * (r + 1) / 2 + c];
 #pragma unroll
           for (int t = 0; t < c; ++t) a -= Lm[r * (r + 1) / 2 + t] * Lm[c * (c + 1) / 2 + t];
           Lm[r * (r + 1) / 2 + c] = a * ig;
         }
       }
-      rt[0] = rv[k * 6 + 0] + ((b00 * p8[0] + b10 * p8[1]) + b20 * p8[2]);
+      rt[0] = (R)rv[k * 6 + 0] + ((b00 * p8[0] + b10 * p8[1]) + b20 * p8[2]);
 #pragma unroll
-      for (int r = 1; r < 6; ++r) rt[r] = rv[k * 6 + r] + T * p8[2 + r];
+      for (int r = 1; r < 6; ++r) rt[r] = (R)rv[k * 6 + r] + Tr * p8[2 + r];
 #pragma unroll
       for (int r = 0; r < 6; ++r) {
-        double a = rt[r];
+        R a = rt[r];
 #pragma unroll
         for (int t = 0; t < r; ++t) a -= Lm[r * (r + 1) / 2 + t] * v[t];
         v[r] = a * idg[r];
       }
 #pragma unroll
       for (int r = 5; r >= 0; --r) {
-        double a = v[r];
+        R a = v[r];
 #pragma unroll
         for (int t = r + 1; t < 6; ++t) a -= Lm[t * (t + 1) / 2 + r] * v[t];
         v[r] = a * idg[r];
       }
       if (lanef() == 0) {
 #pragma unroll
-        for (int r = 0; r < 6; ++r) kf[k * 6 + r] = -v[r];
+        for (int r = 0; r < 6; ++r) kf[k * 6 + r] = (double)(-v[r]);
       }
-      double pn[8];
+      R pn[8];
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
-        double atp = p8[i];
+        R atp = p8[i];
         if (i == 3) atp = atp + ((E03 * p8[0] + E13 * p8[1]) + E23 * p8[2]);
         else if (i == 4) atp = atp + (E04 * p8[0] + E14 * p8[1]);
-        double kr = 0.0;
+        R kr = (R)0;
 #pragma unroll
-        for (int r = 0; r < 6; ++r) kr += K[k * 48 + r * 8 + i] * rt[r];
-        pn[i] = (qs[k * 10 + i] + atp) + kr;
+        for (int r = 0; r < 6; ++r) kr += (R)K[k * 48 + r * 8 + i] * rt[r];
+        pn[i] = ((ZQ ? (R)0 : (R)qs[k * 10 + i]) + atp) + kr;
       }
 #pragma unroll
       for (int i = 0; i < 8; ++i) p8[i] = pn[i];
     }
     sync();
     STAMP1(PH_RESOLVE);
+  }
+
+  // One step of iterative refinement in fp64 of a step (dUo, dXo) solved with the fp32
+  // factorisation (CAP::refine): the U-space residual of the LQ subproblem the factors
+  // came from, res_k = S_k dx_k + R_k du_k + r_k + B_k^T lam_{k+1} with
+  // lam_k = Q_k dx_k + S_k^T du_k + q_k + A_k^T lam_{k+1} (lam_N = Q_N dx_N + q_N), is
+  // formed in fp64 (stage-parallel, adjoint-style suffix sums), solved with the same
+  // factors (resolve with q = 0, r = res) and the correction added.  No-op for fp64.
+  __device__ __forceinline__ void refine(const GLB double* Rd, const GLB double* rv, GLB double* dUo,
+                                         LDS double* dXo) {
+    if constexpr (CAP::refine) {
+      const int k = lanef();
+      LDS double* wv = inc;  // w_k
+      LDS double* lm = Xt;   // lam_k (Xt is free whenever a step is being computed)
+      if (k <= N) {
+        double dx[8], w[8];
+#pragma unroll
+        for (int a = 0; a < 8; ++a) dx[a] = dXo[k * 8 + a];
+#pragma unroll
+        for (int a = 0; a < 8; ++a) {
+          double acc = qs[k * 10 + a];
+#pragma unroll
+          for (int c = 0; c < 8; ++c) acc += Qs[k * 36 + (a <= c ? pk8(a, c) : pk8(c, a))] * dx[c];
+          w[a] = acc;
+        }
+        if (k < N) {
+          const double du0 = dUo[k * 6];
+          w[3] += qs[k * 10 + 8] * du0;
+          w[4] += qs[k * 10 + 9] * du0;
+        }
+#pragma unroll
+        for (int a = 0; a < 8; ++a) wv[k * 8 + a] = w[a];
+      }
+      sync();
+      if (k <= N) {  // components 0,1,2,5,6,7: suffix sums of w (A = I + E, E^T only feeds 3, 4)
+        const int cs[6] = {0, 1, 2, 5, 6, 7};
+#pragma unroll
+        for (int q = 0; q < 6; ++q) {
+          double acc = 0.0;
+          for (int jj = N; jj >= k; --jj) acc += wv[jj * 8 + cs[q]];
+          lm[k * 8 + cs[q]] = acc;
+        }
+      }
+      sync();
+      if (k <= N) {
+        double a3 = wv[N * 8 + 3], a4 = wv[N * 8 + 4];
+        for (int jj = N - 1; jj >= k; --jj) {
+          double E03, E04, E13, E14, E23, b00, b10, b20;
+          stage_AB(jj, E03, E04, E13, E14, E23, b00, b10, b20);
+          const LDS double* ln = lm + (jj + 1) * 8;
+          a3 = wv[jj * 8 + 3] + (((E03 * ln[0] + E13 * ln[1]) + E23 * ln[2]) + a3);
+          a4 = wv[jj * 8 + 4] + ((E04 * ln[0] + E14 * ln[1]) + a4);
+        }
+        lm[k * 8 + 3] = a3;
+        lm[k * 8 + 4] = a4;
+      }
+      sync();
+      if (k < N) {
+        double E03, E04, E13, E14, E23, b00, b10, b20;
+        stage_AB(k, E03, E04, E13, E14, E23, b00, b10, b20);
+        const LDS double* ln = lm + (k + 1) * 8;
+        const LDS double* dxk = dXo + k * 8;
+#pragma unroll
+        for (int c = 0; c < 6; ++c) {
+          double r = rv[k * 6 + c] + (Rd[k * 6 + c] + delta) * dUo[k * 6 + c];
+          r += (c == 0) ? ((b00 * ln[0] + b10 * ln[1]) + b20 * ln[2]) + (qs[k * 10 + 8] * dxk[3] + qs[k * 10 + 9] * dxk[4])
+                        : T * ln[2 + c];
+          rres[k * 6 + c] = (c < nuE) ? r : 0.0;  // absent controls: unit pivot, zero step
+        }
+      }
+      sync();
+      resolve<true>(rres);
+      forward(dUr, rdX);
+      for (int i = lanef(); i < nw; i += WAVE) dUo[i] += dUr[i];
+      for (int i = lanef(); i < 8 * (N + 1); i += WAVE) dXo[i] += rdX[i];
+      sync();
+    }
   }
 
   // forward sweep: du_k = K_k dx_k + k_k ; dx_{k+1} = A_k dx_k + B_k du_k.
@@ -1608,6 +1710,7 @@ __device__ __forceinline__ void resto_phase(const Params* __restrict__ prm, doub
           S.assemble(SUM_LS_RESTO, 0.0, 0.0, false);
           S.riccati(S.sigx, S.ru);
           S.forward(S.dU, S.dX);
+          S.refine(S.sigx, S.ru, S.dU, S.dX);
           double ymax = 0.0;
           for (int r = S.lanef(); r < ng; r += WAVE) {
             const int k = r / m, i = r - k * m;
@@ -1834,6 +1937,7 @@ __device__ __forceinline__ void resto_phase(const Params* __restrict__ prm, doub
         S.delta = dR;
         if (!fok) { rstat = ST_STEP_ERR; break; }
         S.forward(S.dU, S.dX);
+        S.refine(S.sigx, S.ru, S.dU, S.dX);
         {
           STAMP0();
           double th, g;
@@ -1955,6 +2059,7 @@ __device__ __forceinline__ void resto_phase(const Params* __restrict__ prm, doub
               S.assemble(SUM_RESTO_SOC, 0.0, 0.0, true);
               S.resolve(S.ru);
               S.forward(S.dU2, S.dX);
+              S.refine(S.sigx, S.ru, S.dU2, S.dX);
               double t0, t1;
               S.row_step_resto(S.dX, true, S.ds2, S.dp2R, S.dn2R, S.dy2R, t0, t1);
               a_soc = S.frac_to_bound_resto(V[5], S.dU2, S.ds2, S.dp2R, S.dn2R);
@@ -2307,6 +2412,7 @@ __device__ __forceinline__ int solve_one(Solver<CAP>& S, const Params* __restric
       S.assemble(SUM_LS, 0.0, -S.df, false);
       S.riccati(S.sigx, S.ru);
       S.forward(S.dU, S.dX);
+      S.refine(S.sigx, S.ru, S.dU, S.dX);
       double ymax = 0.0;
       for (int r = S.lanef(); r < ng; r += WAVE) {
         // y = bs - J wx with J wx = Gt dX
@@ -2499,6 +2605,7 @@ __device__ __forceinline__ int solve_one(Solver<CAP>& S, const Params* __restric
     S.delta = delta;
     if (!fact_ok) { status = ST_STEP_ERR; break; }
     S.forward(S.dU, S.dX);
+    S.refine(S.sigx, S.ru, S.dU, S.dX);
 
     // ===== line search (BacktrackingLineSearch + FilterLSAcceptor)
     double theta_ref = 0.0, gbd = 0.0, tiny_mx = 0.0, tiny_msv = 0.0;
@@ -2757,6 +2864,7 @@ __device__ __forceinline__ int solve_one(Solver<CAP>& S, const Params* __restric
               S.assemble(SUM_SOC, S.df, S.df, true);
               S.resolve(S.ru);
               S.forward(S.dU2, S.dX);   // dX is free once gBD is known
+              S.refine(S.sigx, S.ru, S.dU2, S.dX);
               S.row_step(S.dX, S.dms, true, S.ds2);
               a_soc = S.frac_to_bound(tau, S.dU2, S.ds2);
               dsp = S.ds2;
@@ -3272,10 +3380,15 @@ struct ClassFns {
 ClassFns nmpc_class_fns_A();
 ClassFns nmpc_class_fns_B();
 ClassFns nmpc_class_fns_C();
+ClassFns nmpc_class_fns_A32();
+ClassFns nmpc_class_fns_C32();
 
 using CapA = Cap<20, 15, true>;   // BASELINE configs 2-4 (N=20, <=10 obstacles) and the reference's N=15 scripts
 using CapB = Cap<31, 21>;
 using CapC = Cap<63, 21>;   // any supported shape
+// fp32 Riccati factorisation (nmpc_options.linear_solver_fp32; BASELINE config 5's fp32 leg)
+using CapA32 = Cap<20, 15, true, float>;
+using CapC32 = Cap<63, 21, false, float>;
 
 #ifdef NMPC_TU_CLASS
 template <class CAP>
@@ -3287,8 +3400,12 @@ static ClassFns class_fns() {
 ClassFns nmpc_class_fns_A() { return class_fns<CapA>(); }
 #elif NMPC_TU_CLASS == 2
 ClassFns nmpc_class_fns_B() { return class_fns<CapB>(); }
-#else
+#elif NMPC_TU_CLASS == 3
 ClassFns nmpc_class_fns_C() { return class_fns<CapC>(); }
+#elif NMPC_TU_CLASS == 4
+ClassFns nmpc_class_fns_A32() { return class_fns<CapA32>(); }
+#else
+ClassFns nmpc_class_fns_C32() { return class_fns<CapC32>(); }
 #endif
 #else  // host translation unit
 
@@ -3326,7 +3443,9 @@ struct nmpc_handle {
 
 static void pick_class(const Params& P, KernFn* fn, LoopFn* lfn, SchedFn* sfn, int* lds_doubles, int* ws_doubles) {
   ClassFns c;
-  if (P.N <= CapA::nmax && P.m <= CapA::mmax) c = nmpc_class_fns_A();
+  const bool fit_a = P.N <= CapA::nmax && P.m <= CapA::mmax;
+  if (P.o.linear_solver_fp32) c = fit_a ? nmpc_class_fns_A32() : nmpc_class_fns_C32();
+  else if (fit_a) c = nmpc_class_fns_A();
   else if (P.N <= CapB::nmax && P.m <= CapB::mmax) c = nmpc_class_fns_B();
   else c = nmpc_class_fns_C();
   *fn = c.fn; *lfn = c.lfn; *sfn = c.sfn; *lds_doubles = c.lds_doubles; *ws_doubles = c.ws_doubles;

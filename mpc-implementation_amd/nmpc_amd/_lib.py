@@ -28,7 +28,7 @@ EXPORTS = (
 )
 
 _OPT_INT = ("max_iter", "acceptable_iter", "max_soc", "max_soft_resto_iters",
-            "watchdog_shortened_iter_trigger", "watchdog_trial_iter_max")
+            "watchdog_shortened_iter_trigger", "watchdog_trial_iter_max", "linear_solver_fp32", "reserved0")
 _OPT_DBL = (
     "tol", "acceptable_tol", "acceptable_obj_change_tol", "acceptable_dual_inf_tol",
     "acceptable_constr_viol_tol", "acceptable_compl_inf_tol",

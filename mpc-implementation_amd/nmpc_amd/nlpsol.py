@@ -51,6 +51,8 @@ def make_options(opts: dict | None) -> _lib.Options:
     if not opts:
         return o
     ip = dict(opts.get("ipopt", {}))
+    if "linear_solver_fp32" in ip or "reserved0" in ip:
+        raise ValueError("use the nlpsol option linear_solver_precision='single' (not an IPOPT option)")
     for k, v in ip.items():
         name = _lib.IPOPT_ALIASES.get(k, k)
         if name in ("print_level", "print_timing_statistics", "sb", "linear_solver", "hessian_approximation",
@@ -66,8 +68,12 @@ def make_options(opts: dict | None) -> _lib.Options:
             raise ValueError(f"unsupported IPOPT option {k!r}")
         setattr(o, name, type(getattr(o, name))(v))
     for k in opts:
-        if k not in ("ipopt", "print_time", "verbose", "expand", "error_on_fail"):
+        if k not in ("ipopt", "print_time", "verbose", "expand", "error_on_fail", "linear_solver_precision"):
             raise ValueError(f"unsupported nlpsol option {k!r}")
+    prec = opts.get("linear_solver_precision", "double")
+    if prec not in ("double", "single"):
+        raise ValueError("linear_solver_precision must be 'double' or 'single'")
+    o.linear_solver_fp32 = 1 if prec == "single" else 0
     return o
 
 
