@@ -21,6 +21,8 @@
  *   lbg, ubg, g_out, lam_g_out     : ng x B column-major, ng = (5+n_obs)*(N+1)
  *   p                              : np x B column-major, p = [x0(8); xs(3); dynamic obstacle coords]
  *   X_out                          : 8*(N+1) x B column-major  (ff(u, p), Python/NMPC_TT.py:169)
+ *   lam_p_out                      : np x B column-major, -grad_p (f + lam_g' g) at x_out
+ *                                    (CasADi nlpsol's lam_p; nullable)
  * A leading dimension of 0 broadcasts one column to every scenario (bounds
  * are normally shared: Python/NMPC_TT.py:269-306).  +-inf (|b| >= 1e19)
  * means "no bound", as ca.inf does (Python/NMPC_TT.py:280-282).
@@ -139,7 +141,7 @@ int nmpc_solve_batch(nmpc_handle* h, int32_t B,
                      const double* lbg, int64_t ld_lbg, const double* ubg, int64_t ld_ubg,
                      const double* p, int64_t ld_p,
                      double* x_out, double* f_out, double* g_out,
-                     double* lam_x_out, double* lam_g_out, double* X_out,
+                     double* lam_x_out, double* lam_g_out, double* lam_p_out, double* X_out,
                      int32_t* status, int32_t* iters);
 
 /* Same with DEVICE pointers, enqueued on `stream` (hipStream_t; NULL = default
@@ -150,7 +152,7 @@ int nmpc_solve_batch_dev(nmpc_handle* h, int32_t B,
                          const double* lbg, int64_t ld_lbg, const double* ubg, int64_t ld_ubg,
                          const double* p, int64_t ld_p,
                          double* x_out, double* f_out, double* g_out,
-                         double* lam_x_out, double* lam_g_out, double* X_out,
+                         double* lam_x_out, double* lam_g_out, double* lam_p_out, double* X_out,
                          int32_t* status, int32_t* iters, void* stream);
 
 /* Optional per-iteration trace (debugging / parity): when enabled, the next

@@ -162,7 +162,7 @@ struct Cap {
 struct IO {
   const double *x0, *lbx, *ubx, *lbg, *ubg, *p;
   long long ld_x0, ld_lbx, ld_ubx, ld_lbg, ld_ubg, ld_p;
-  double *x_out, *f_out, *g_out, *lam_x, *lam_g, *X_out;
+  double *x_out, *f_out, *g_out, *lam_x, *lam_g, *lam_p, *X_out;
   int *status, *iters;
   double* trace;
   double* ws;  // per-scenario global workspace, B x wstotal
@@ -3027,6 +3027,59 @@ __device__ __forceinline__ int solve_one(Solver<CAP>& S, const Params* __restric
     if (io.g_out) io.g_out[(long long)b * ng + r] = S.dt[r];
     if (io.lam_g) io.lam_g[(long long)b * ng + r] = S.y[r] * S.dc[r] / S.df;
   }
+  if (io.lam_p) {
+    // lam_p = -grad_p (f + lam_g' g) at the returned point (CasADi nlpsol's lam_p; the
+    // reference never reads it): x0 through the Lagrangian adjoint of the rollout, the
+    // target through the stage costs, moving obstacles through their rows, cost weights
+    // taken from p through the cost terms they scale
+    for (int i = S.lanef(); i < prm->nX; i += WAVE) S.X[i] = S.Xt[i];
+    sync();
+    S.derivs(S.X, S.Ut);
+    S.adjoint(S.df, S.y);  // lam_k = df * dL/dx_k  (lam_g = y dc / df)
+    const int k = S.lanef();
+    const double gxt = -wsum(k < N ? S.gl[k * 8] : 0.0), gyt = -wsum(k < N ? S.gl[k * 8 + 1] : 0.0);
+    double g_w1 = 0.0, g_w2 = 0.0;
+    if (prm->w1p >= 0 || prm->w2p >= 0) {
+      const double w1s = S.rvars[30], w2s = S.rvars[31];
+      sync();
+      S.rvars[30] = 1.0; S.rvars[31] = 0.0;
+      sync();
+      const double cd = k < N ? S.stage_cost(S.X + k * 8) : 0.0;
+      sync();
+      S.rvars[30] = 0.0; S.rvars[31] = 1.0;
+      sync();
+      const double cq = k < N ? S.stage_cost(S.X + k * 8) : 0.0;
+      sync();
+      S.rvars[30] = w1s; S.rvars[31] = w2s;
+      sync();
+      g_w1 = wsum(cd); g_w2 = wsum(cq);
+    }
+    const int np = prm->np;
+    double v = 0.0;
+    if (k < 8) v = S.lam[k] / S.df;
+    else if (k == 8) v = gxt;
+    else if (k == 9) v = gyt;
+    if (k == prm->w1p) v += g_w1;
+    if (k == prm->w2p) v += g_w2;
+    for (int o = 0; o < S.nobs; ++o) {
+      if (prm->oxp[o] < 0 && prm->oyp[o] < 0) continue;
+      double cx = 0.0, cy = 0.0;
+      if (k <= N) {  // row g = r_sum - |(x, y) - (ox, oy)|: dg/dox = (x - ox) / d
+        const int r = k * S.m + S.nb + o;
+        const double lg = S.y[r] * S.dc[r] / S.df;
+        const LDS double* xk = S.X + k * 8;
+        const double ddx = xk[0] - S.obx[o], ddy = xk[1] - S.oby[o];
+        const double idd = rsq(ddx * ddx + ddy * ddy);
+        cx = lg * (ddx * idd);
+        cy = lg * (ddy * idd);
+      }
+      cx = wsum(cx); cy = wsum(cy);
+      if (k == prm->oxp[o]) v += cx;
+      if (k == prm->oyp[o]) v += cy;
+    }
+    const int e = k < np ? ext_p(prm, k) : -1;
+    if (e >= 0) io.lam_p[(long long)b * prm->npE + e] = -v;
+  }
   if (io.X_out) {
     const int nX = prm->nX, nxE = prm->nxE, nXE = nxE * (N + 1);
     for (int i = S.lanef(); i < nX; i += WAVE) {
@@ -3631,8 +3684,8 @@ int nmpc_read_trace(nmpc_handle* h, int32_t B, double* host_out) {
 int nmpc_solve_batch_dev(nmpc_handle* h, int32_t B, const double* x0, int64_t ld_x0, const double* lbx,
                          int64_t ld_lbx, const double* ubx, int64_t ld_ubx, const double* lbg, int64_t ld_lbg,
                          const double* ubg, int64_t ld_ubg, const double* p, int64_t ld_p, double* x_out,
-                         double* f_out, double* g_out, double* lam_x_out, double* lam_g_out, double* X_out,
-                         int32_t* status, int32_t* iters, void* stream) {
+                         double* f_out, double* g_out, double* lam_x_out, double* lam_g_out, double* lam_p_out,
+                         double* X_out, int32_t* status, int32_t* iters, void* stream) {
   if (!h) return fail(NMPC_E_INVALID, "null handle");
   if (B < 0) return fail(NMPC_E_INVALID, "B < 0");
   if (B == 0) return NMPC_OK;
@@ -3646,6 +3699,7 @@ int nmpc_solve_batch_dev(nmpc_handle* h, int32_t B, const double* x0, int64_t ld
   io.x0 = x0; io.lbx = lbx; io.ubx = ubx; io.lbg = lbg; io.ubg = ubg; io.p = p;
   io.ld_x0 = ld_x0; io.ld_lbx = ld_lbx; io.ld_ubx = ld_ubx; io.ld_lbg = ld_lbg; io.ld_ubg = ld_ubg; io.ld_p = ld_p;
   io.x_out = x_out; io.f_out = f_out; io.g_out = g_out; io.lam_x = lam_x_out; io.lam_g = lam_g_out;
+  io.lam_p = lam_p_out;
   io.X_out = X_out; io.status = status; io.iters = iters; io.trace = nullptr;
   if (h->trace) {
     const size_t need = (size_t)B * (P.o.max_iter + 3) * TRACE_F * sizeof(double);
@@ -3671,7 +3725,8 @@ int nmpc_solve_batch_dev(nmpc_handle* h, int32_t B, const double* x0, int64_t ld
 int nmpc_solve_batch(nmpc_handle* h, int32_t B, const double* x0, int64_t ld_x0, const double* lbx, int64_t ld_lbx,
                      const double* ubx, int64_t ld_ubx, const double* lbg, int64_t ld_lbg, const double* ubg,
                      int64_t ld_ubg, const double* p, int64_t ld_p, double* x_out, double* f_out, double* g_out,
-                     double* lam_x_out, double* lam_g_out, double* X_out, int32_t* status, int32_t* iters) {
+                     double* lam_x_out, double* lam_g_out, double* lam_p_out, double* X_out, int32_t* status,
+                     int32_t* iters) {
   if (!h) return fail(NMPC_E_INVALID, "null handle");
   if (B < 0) return fail(NMPC_E_INVALID, "B < 0");
   if (B == 0) return NMPC_OK;
@@ -3684,7 +3739,7 @@ int nmpc_solve_batch(nmpc_handle* h, int32_t B, const double* x0, int64_t ld_x0,
   const size_t n_x0 = len(ld_x0, nw), n_lbx = len(ld_lbx, nw), n_ubx = len(ld_ubx, nw);
   const size_t n_lbg = len(ld_lbg, ng), n_ubg = len(ld_ubg, ng), n_p = len(ld_p, np);
   (void)cols;
-  const size_t n_out = (size_t)B * (2 * nw + 2 * ng + nX + 1);
+  const size_t n_out = (size_t)B * (2 * nw + 2 * ng + nX + np + 1);
   const size_t total = n_x0 + n_lbx + n_ubx + n_lbg + n_ubg + n_p + n_out;
   if (total * sizeof(double) > h->dbuf_bytes) {
     if (h->dbuf) hipFree(h->dbuf);
@@ -3710,6 +3765,7 @@ int nmpc_solve_batch(nmpc_handle* h, int32_t B, const double* x0, int64_t ld_x0,
   double* d_g = q; q += (size_t)B * ng;
   double* d_lg = q; q += (size_t)B * ng;
   double* d_X = q; q += (size_t)B * nX;
+  double* d_lp = q; q += (size_t)B * np;
   double* d_f = q; q += (size_t)B;
   int* d_st = h->ibuf;
   int* d_it = h->ibuf + B;
@@ -3721,7 +3777,8 @@ int nmpc_solve_batch(nmpc_handle* h, int32_t B, const double* x0, int64_t ld_x0,
   up(d_lbg, lbg, n_lbg); up(d_ubg, ubg, n_ubg); up(d_p, p, n_p);
   if (e != hipSuccess) return fail(NMPC_E_HIP, std::string("hipMemcpy H2D: ") + hipGetErrorString(e));
   int rc = nmpc_solve_batch_dev(h, B, d_x0, ld_x0, d_lbx, ld_lbx, d_ubx, ld_ubx, d_lbg, ld_lbg, d_ubg, ld_ubg,
-                                d_p, ld_p, d_x, d_f, d_g, d_lx, d_lg, d_X, d_st, d_it, nullptr);
+                                d_p, ld_p, d_x, d_f, d_g, d_lx, d_lg, lam_p_out ? d_lp : nullptr, d_X, d_st, d_it,
+                                nullptr);
   if (rc != NMPC_OK) return rc;
   e = hipDeviceSynchronize();
   if (e != hipSuccess) return fail(NMPC_E_HIP, std::string("kernel: ") + hipGetErrorString(e));
@@ -3731,6 +3788,7 @@ int nmpc_solve_batch(nmpc_handle* h, int32_t B, const double* x0, int64_t ld_x0,
   down(x_out, d_x, (size_t)B * nw * 8); down(lam_x_out, d_lx, (size_t)B * nw * 8);
   down(g_out, d_g, (size_t)B * ng * 8); down(lam_g_out, d_lg, (size_t)B * ng * 8);
   down(X_out, d_X, (size_t)B * nX * 8); down(f_out, d_f, (size_t)B * 8);
+  down(lam_p_out, d_lp, (size_t)B * np * 8);
   down(status, d_st, (size_t)B * 4); down(iters, d_it, (size_t)B * 4);
   if (e != hipSuccess) return fail(NMPC_E_HIP, std::string("hipMemcpy D2H: ") + hipGetErrorString(e));
   return NMPC_OK;

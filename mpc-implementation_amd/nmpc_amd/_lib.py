@@ -91,9 +91,9 @@ def lib():
     L.nmpc_create.argtypes = [C.POINTER(Desc), C.POINTER(vp)]
     L.nmpc_destroy.argtypes = [vp]
     L.nmpc_dims.argtypes = [vp, i32p, i32p, i32p, i32p]
-    args = [vp, C.c_int32] + [dp, i64] * 6 + [dp] * 6 + [i32p, i32p]
+    args = [vp, C.c_int32] + [dp, i64] * 6 + [dp] * 7 + [i32p, i32p]
     L.nmpc_solve_batch.argtypes = args
-    L.nmpc_solve_batch_dev.argtypes = [vp, C.c_int32] + [vp, i64] * 6 + [vp] * 6 + [vp, vp, vp]
+    L.nmpc_solve_batch_dev.argtypes = [vp, C.c_int32] + [vp, i64] * 6 + [vp] * 7 + [vp, vp, vp]
     L.nmpc_set_trace.argtypes = [vp, C.c_int32]
     L.nmpc_read_trace.argtypes = [vp, C.c_int32, dp]
     L.nmpc_shift_dev.argtypes = [vp, C.c_int32, vp, i64, vp, vp, vp, vp, vp]

@@ -55,6 +55,11 @@ def make_options(opts: dict | None) -> _lib.Options:
         raise ValueError("use the nlpsol option linear_solver_precision='single' (not an IPOPT option)")
     for k, v in ip.items():
         name = _lib.IPOPT_ALIASES.get(k, k)
+        if name == "warm_start_init_point":
+            if v != "no":
+                raise ValueError("only warm_start_init_point='no' (IPOPT default: lam_x0/lam_g0 unused) "
+                                 "is supported")
+            continue
         if name in ("print_level", "print_timing_statistics", "sb", "linear_solver", "hessian_approximation",
                     "mu_strategy", "nlp_scaling_method", "fixed_variable_treatment"):
             if name == "hessian_approximation" and v != "exact":
@@ -131,10 +136,15 @@ class Solver:
             return cols, n
         raise ValueError(f"{name}: expected a vector or an (n,B) matrix")
 
-    def __call__(self, x0=None, lbx=None, ubx=None, lbg=None, ubg=None, p=None, **kw):
-        for k in kw:
-            if k not in ("lam_x0", "lam_g0"):
-                raise ValueError(f"unknown argument {k!r}")
+    def __call__(self, x0=None, lbx=None, ubx=None, lbg=None, ubg=None, p=None, lam_x0=None, lam_g0=None):
+        # lam_x0 / lam_g0 are accepted and, exactly as IPOPT does under its default
+        # warm_start_init_point='no' (the reference sets no warm-start option,
+        # Python/NMPC_TT.py:257-265), not used: the multipliers are initialised by
+        # IPOPT's own rules (bound_mult_init_val, least-squares y).  Their shapes are
+        # still checked as CasADi checks them.
+        for name, v, n in (("lam_x0", lam_x0, self.nw), ("lam_g0", lam_g0, self.ng)):
+            if v is not None:
+                self._arg(v, n, 0.0, name)
         args = {}
         B = 1
         for name, v, n, dflt in (("x0", x0, self.nw, 0.0), ("lbx", lbx, self.nw, -np.inf),
@@ -149,11 +159,10 @@ class Solver:
         out = self.solve_batch(B, **{k: v for k, v in args.items()})
         single = B == 1
         res = {}
-        for k in ("x", "g", "lam_x", "lam_g", "X"):
+        for k in ("x", "g", "lam_x", "lam_g", "lam_p", "X"):
             arr = out[k].T  # (n, B)
             res[k] = arr if not single else arr.reshape(-1, 1)
         res["f"] = out["f"].reshape(1, B) if not single else out["f"].reshape(1, 1)
-        res["lam_p"] = np.full((self.np, B) if not single else (self.np, 1), np.nan)  # not computed
         st = out["status"]
         self._stats = {
             "return_status": RETURN_STATUS.get(int(st[0]), str(int(st[0]))) if single
@@ -171,7 +180,8 @@ class Solver:
         L = _lib.lib()
         out = {
             "x": np.empty((B, self.nw)), "g": np.empty((B, self.ng)), "lam_x": np.empty((B, self.nw)),
-            "lam_g": np.empty((B, self.ng)), "X": np.empty((B, self.nX)), "f": np.empty(B),
+            "lam_g": np.empty((B, self.ng)), "lam_p": np.empty((B, self.np)), "X": np.empty((B, self.nX)),
+            "f": np.empty(B),
             "status": np.empty(B, dtype=np.int32), "iters": np.empty(B, dtype=np.int32),
         }
         ins = []
@@ -179,7 +189,7 @@ class Solver:
             ins += [_dptr(a), ld]
         _lib.check(L.nmpc_solve_batch(
             self._h, B, *ins, _dptr(out["x"]), _dptr(out["f"]), _dptr(out["g"]), _dptr(out["lam_x"]),
-            _dptr(out["lam_g"]), _dptr(out["X"]), out["status"].ctypes.data_as(_IP),
+            _dptr(out["lam_g"]), _dptr(out["lam_p"]), _dptr(out["X"]), out["status"].ctypes.data_as(_IP),
             out["iters"].ctypes.data_as(_IP)))
         return out
 
@@ -187,7 +197,7 @@ class Solver:
         """Device path: torch CUDA float64 tensors, scenario-major (B, n) or shared (n,).
 
         ``out`` holds preallocated device tensors x (B,nw) [required], f (B,),
-        g (B,ng), lam_x (B,nw), lam_g (B,ng), X (B,nX), status/iters (B,) int32
+        g (B,ng), lam_x (B,nw), lam_g (B,ng), lam_p (B,np), X (B,nX), status/iters (B,) int32
         (optional).  Enqueued on ``stream`` (torch stream; default = current).
         """
         import torch  # plumbing only: device memory and streams
@@ -214,7 +224,7 @@ class Solver:
         if stream is None:
             stream = torch.cuda.current_stream()
         _lib.check(L.nmpc_solve_batch_dev(self._h, B, *ins, op("x"), op("f"), op("g"), op("lam_x"),
-                                          op("lam_g"), op("X"), op("status"), op("iters"),
+                                          op("lam_g"), op("lam_p"), op("X"), op("status"), op("iters"),
                                           C.c_void_p(stream.cuda_stream)))
 
     def shift_device(self, p, u_sol, w_out, v_t, w_t, stream=None):

@@ -287,6 +287,23 @@ def constraints(prob, w, p):
     return np.concatenate([stage_rows(prob, X[:, k], ox, oy) for k in range(prob.N + 1)])
 
 
+def lam_p(prob, w, p, lam_g, h=1e-6):
+    """CasADi nlpsol's lam_p = -grad_p (f + lam_g' g) at (w, p), by central differences
+    of objective() / constraints() (checker for the kernel's analytic lam_p; relative
+    step h, accuracy ~h^2 plus rounding)."""
+    p = np.asarray(p, dtype=float)
+    out = np.zeros_like(p)
+    for i in range(len(p)):
+        d = h * max(1.0, abs(p[i]))
+        pp, pm = p.copy(), p.copy()
+        pp[i] += d
+        pm[i] -= d
+        Lp = objective(prob, w, pp) + lam_g @ constraints(prob, w, pp)
+        Lm = objective(prob, w, pm) + lam_g @ constraints(prob, w, pm)
+        out[i] = -(Lp - Lm) / (2 * d)
+    return out
+
+
 # --- hand-derived derivatives ------------------------------------------------
 _V = [0, 1, 2, 5, 6, 7]  # state indices the stage cost depends on
 

@@ -166,7 +166,7 @@ def test_empty_batch_is_noop():
     from nmpc_amd import _lib, make_spec
 
     s = _solver(make_spec(None, N=4, T=0.2))
-    assert _lib.lib().nmpc_solve_batch(s._h, 0, *([None, 0] * 6), *([None] * 6), None, None) == 0
+    assert _lib.lib().nmpc_solve_batch(s._h, 0, *([None, 0] * 6), *([None] * 7), None, None) == 0
 
 
 @pytest.mark.parametrize("N,layout", [(1, "race_track_2"), (63, None)])
@@ -737,3 +737,38 @@ def test_step_queue_guard_reports_unrun_scenarios():
     assert np.all(st[:, pos % 8 == 0] != NOT_RUN) and np.all(st != 99)
     assert np.isnan(hist["f"].cpu().numpy()[:, pos % 8 != 0]).all()
     assert info["steps_done"] == K * int((pos % 8 == 0).sum())
+
+
+@pytest.mark.parametrize("layout,N,dyn,model,weights", [("race_track_2", 12, False, "uav8g", False),
+                                                         ("dynamic", 10, True, "uav8g", False),
+                                                         ("race_track_2", 10, False, "uav8g", True),
+                                                         ("10_obstacles", 8, False, "uav5", False)])
+def test_lam_p_matches_oracle_finite_differences(layout, N, dyn, model, weights):
+    """lam_p = -grad_p (f + lam_g' g) at the returned x (CasADi nlpsol's output; the
+    reference never reads it): x0 through the adjoint of the rollout, the target through
+    the stage costs, moving-obstacle coordinates and cost weights taken from p --
+    against central differences of the oracle's objective / constraints at the GPU's
+    own (x, lam_g).  Parity unpinned against CasADi itself (not installed); the sign
+    follows CasADi's convention grad f + J_g' lam_g + lam_x = 0 extended to p."""
+    from nmpc_amd import make_spec, draw_scenarios
+
+    spec = make_spec(layout, N=N, T=0.2, dynamic=dyn, model=model, weights_in_p=weights)
+    P = draw_scenarios(make_spec(layout, N=N, T=0.2, dynamic=dyn, model=model), 4, seed=21)
+    prob = orc.make_problem(layout, N=N, T=0.2, dynamic=dyn, model=model)
+    if weights:
+        P = np.hstack([P, np.array([[1.0, 2.0], [0.5, 3.0], [2.0, 0.5], [1.5, 1.0]])])
+        prob.w1_pidx, prob.w2_pidx, prob.np_ = P.shape[1] - 2, P.shape[1] - 1, P.shape[1]
+    s = _solver(spec)
+    lbx, ubx, lbg, ubg = spec.bounds()
+    sol = s(x0=np.zeros(spec.nw), lbx=lbx, ubx=ubx, lbg=lbg, ubg=ubg, p=P.T)
+    st = s.stats()["status_code"]
+    checked = 0
+    for b in range(4):
+        if st[b] not in (0, 1):
+            continue
+        ref = orc.lam_p(prob, sol["x"][:, b], P[b], sol["lam_g"][:, b])
+        got = sol["lam_p"][:, b]
+        scale = 1.0 + np.abs(ref).max()
+        assert np.all(np.abs(got - ref) <= 1e-5 * scale), (b, got, ref)
+        checked += 1
+    assert checked >= 2
