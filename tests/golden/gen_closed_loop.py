@@ -11,6 +11,10 @@ x, f).  The GPU tests (tests/test_gpu.py) use them two ways:
     until the two loops first take a different branch.
 
 Cases (SURVEY 8(d) distributions via nmpc_amd.draw_scenarios):
+  config1 : BASELINE config 1 (no-gimbal model of MATLAB/Dynamic Obstacles/NMPC_TT.m,
+            N=10, no obstacles), seed 1001, 32 scenarios x 10 warm-started steps;
+  config2 : BASELINE config 2 (N=20, no obstacles, T=0.2), seed 1002, 32 scenarios
+            x 10 warm-started steps;
   config3 : BASELINE config 3 (N=20, Race Track 2 obstacles, T=0.2), seed 1003,
             the first 64 scenarios, 20 warm-started steps from u = 0, target
             controls (12, 0.01) (Python/NMPC_TT.py:25) -- the bench's workload;
@@ -20,7 +24,7 @@ Cases (SURVEY 8(d) distributions via nmpc_amd.draw_scenarios):
             MATLAB/Dynamic Obstacles/Dynamic Obstacle avoidance.m:213-230 from
             MPC iteration 195 (obstacles 2 and 3 move).
 
-    python tests/golden/gen_closed_loop.py [config3|config5|all] [--procs 8]
+    python tests/golden/gen_closed_loop.py [config1|config2|config3|config5|all] [--procs 8]
 """
 import argparse
 import multiprocessing as mp
@@ -37,6 +41,8 @@ sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "mpc-implementation_amd"))
 
 CASES = {
+    "config1": dict(cfg=1, seed=1001, B=32, K=10, cold=0, it0=0),
+    "config2": dict(cfg=2, seed=1002, B=32, K=10, cold=0, it0=0),
     "config3": dict(cfg=3, seed=1003, B=64, K=20, cold=0, it0=0),
     "config5": dict(cfg=5, seed=1005, B=16, K=10, cold=16, it0=195),
 }

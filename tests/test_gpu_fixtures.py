@@ -1,7 +1,8 @@
 """GPU parity against the oracle's closed-loop fixtures (tests/golden/gen_closed_loop.py):
-BASELINE config 3 (the bench's workload: N=20, 10 obstacles, 64 scenarios x 20
-warm-started MPC steps) and config 5 (N=50, dynamic obstacles moving per
-MATLAB/Dynamic Obstacles/Dynamic Obstacle avoidance.m:213-230; 16 cold solves and
+BASELINE config 1 (no-gimbal model, N=10, 32 scenarios x 10 steps), config 2 (N=20,
+no obstacles, 32 x 10), config 3 (the bench's workload: N=20, 10 obstacles, 64
+scenarios x 20 warm-started MPC steps) and config 5 (N=50, dynamic obstacles moving
+per MATLAB/Dynamic Obstacles/Dynamic Obstacle avoidance.m:213-230; 16 cold solves and
 16 scenarios x 10 warm-started steps).
 
 Two comparisons per case:
@@ -64,7 +65,7 @@ def _per_step(name):
     return same, conv, ok_x, it == oit
 
 
-@pytest.mark.parametrize("name", ["config3", "config5"])
+@pytest.mark.parametrize("name", ["config1", "config2", "config3", "config5"])
 def test_per_step_parity_with_oracle_fixture(name):
     same, conv, ok_x, same_it = _per_step(name)
     assert same.mean() >= 0.95
@@ -90,7 +91,7 @@ def test_config5_cold_solves_match_oracle():
         assert np.all(_relerr(sol["x"].T[conv], z["cold_x"][conv]) <= TOL)
 
 
-@pytest.mark.parametrize("name", ["config3", "config5"])
+@pytest.mark.parametrize("name", ["config1", "config2", "config3", "config5"])
 def test_chained_closed_loop_matches_oracle_fixture(name):
     import torch
 
