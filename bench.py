@@ -385,7 +385,9 @@ def main():
             "value": value, "unit": "MPC steps/s", "n_gpus": world, "steps": K,
             "warmup": W, "ms_per_step": ms_per_step, "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
-            "config": {"workload": f"config {args.config}: batch={B}/GPU, "
+            "config": {"workload": (f"config 4 family: {B * world} scenarios sharded {B}/GPU over {world} GPUs, "
+                                    if world > 1 and args.config == 3 else "")
+                                   + f"config {args.config}: batch={B}/GPU, "
                                    f"{'no-gimbal 5-state' if spec.model == 'uav5' else '8-state UAV+gimbal'}, "
                                    f"N={spec.N}, {spec.n_obs} static obstacles"
                                    f"{' (Race Track 2.py layout)' if spec.n_obs else ''}, T={spec.T}, "
