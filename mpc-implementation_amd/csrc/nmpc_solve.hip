@@ -104,7 +104,11 @@ constexpr Lay make_layout(int N, int m, bool lr, bool refine) {
     L.s = g; g += al8(ng); L.y = g; g += al8(ng); L.vl = g; g += al8(ng); L.vu = g; g += al8(ng);
     L.d = g; g += al8(ng); L.ds = g; g += al8(ng); L.ds2 = g; g += al8(ng); L.dc = g; g += al8(ng);
   }
-  L.dt = g; g += al8(ng); L.dms = g; g += al8(ng);
+  // trial row values: in LDS with the hot rows (not in the refinement classes, whose
+  // LDS budget holds the refinement's step instead)
+  const bool ldt = lr && !refine;
+  if (!ldt) { L.dt = g; g += al8(ng); }
+  L.dms = g; g += al8(ng);
   L.filt = g; g += al8(2 * FCAP + 2);
   L.gl = g; g += al8(8 * NS); L.Hl = g; g += al8(21 * NS); L.Qs = g; g += al8(36 * NS);
   L.K = g; g += al8(48 * N); L.Rk = g; g += al8(21 * N);
@@ -123,8 +127,18 @@ constexpr Lay make_layout(int N, int m, bool lr, bool refine) {
   L.X = o; o += al2(nX); L.Xt = o; o += al2(nX); L.dX = o; o += al2(nX);
   L.trig = o; o += al2(8 * NS); L.qs = o; o += al2(10 * NS); L.lam = o; o += al2(8 * NS);
   L.kf = o; o += al2(6 * N); L.Rc = o; o += 22;
-  L.P0 = o; o += 64; L.P1 = o; o += 64; L.pv0 = o; o += 8; L.pv1 = o; o += 8; L.St = o; o += 48;
-  L.p = o; o += 64; L.ob = o; o += al2(2 * NMPC_MAX_OBS); L.inc = o; o += al2(8 * NS); L.red = o; o += 24;
+  // the Riccati sweep's P / p double buffers: inside `inc` (rollout / adjoint scratch,
+  // never live during the sweep) for the LDS-row classes, separate otherwise
+  const bool pin = lr && 8 * NS >= 144;
+  if (!pin) { L.P0 = o; o += 64; L.P1 = o; o += 64; L.pv0 = o; o += 8; L.pv1 = o; o += 8; }
+  L.St = o; o += 48;
+  L.p = o; o += 64; L.ob = o; o += al2(2 * NMPC_MAX_OBS); L.inc = o; o += al2(8 * NS);
+  if (pin) { L.P0 = L.inc; L.P1 = L.inc + 64; L.pv0 = L.inc + 128; L.pv1 = L.inc + 136; }
+#ifdef NMPC_STAMPS
+  L.red = o; o += 24;  // phase timers
+#else
+  L.red = o;
+#endif
   L.dl = o; o += al2(ng); L.du = o; o += al2(ng);  // row bounds (constant during a solve, read by every row pass)
   L.rvars = o; o += 48;  // line-search / restoration scalars; [32..36] barrier sums; [40..45] watchdog
   L.rdX = o; if (refine) o += al2(nX);  // refinement step in X (fp32 classes)
@@ -132,6 +146,7 @@ constexpr Lay make_layout(int N, int m, bool lr, bool refine) {
     L.s = o; o += al2(ng); L.y = o; o += al2(ng); L.vl = o; o += al2(ng); L.vu = o; o += al2(ng);
     L.d = o; o += al2(ng); L.ds = o; o += al2(ng); L.ds2 = o; o += al2(ng); L.dc = o; o += al2(ng);
   }
+  if (ldt) { L.dt = o; o += al2(ng); }
   L.total = o;
   return L;
 }
@@ -334,7 +349,9 @@ struct Solver {
   LDS double* X, *Xt, *dX;
   using RV = typename CAP::RowT;  // hot row vectors: LDS or global (Cap::lds_rows)
   RV *s, *y, *vl, *vu, *d, *ds, *ds2, *dc;
-  GLB double *dt, *dms;
+  using DTT = std::conditional_t<CAP::lds_rows && !CAP::refine, LDS double, GLB double>;
+  DTT* dt;
+  GLB double* dms;
   GLB double *UR, *zl0, *zu0, *s0, *vl0, *vu0, *pR, *nR, *zpR, *znR, *dpR, *dnR, *dyR, *dp2R, *dn2R, *dy2R, *cms, *filtR;
   GLB double *accU, *accZl, *accZu, *accY;
   GLB double *wU, *wzl, *wzu, *wdU, *wsl, *wy, *wvl, *wvu, *wds, *wpR, *wnR, *wzpR, *wznR, *wdpR, *wdnR, *wdyR;
@@ -368,7 +385,9 @@ struct Solver {
       else return (RV*)(gw + off);
     };
     s = rvp(L.s); y = rvp(L.y); vl = rvp(L.vl); vu = rvp(L.vu);
-    d = rvp(L.d); dt = gw + L.dt; ds = rvp(L.ds); ds2 = rvp(L.ds2);
+    d = rvp(L.d); ds = rvp(L.ds); ds2 = rvp(L.ds2);
+    if constexpr (CAP::lds_rows && !CAP::refine) dt = (DTT*)(sm + L.dt);
+    else dt = (DTT*)(gw + L.dt);
     dc = rvp(L.dc); dl = sm + L.dl; du = sm + L.du; dms = gw + L.dms; rvars = sm + L.rvars;
     UR = gw + L.UR; zl0 = gw + L.zl0; zu0 = gw + L.zu0; s0 = gw + L.s0; vl0 = gw + L.vl0; vu0 = gw + L.vu0;
     pR = gw + L.pR; nR = gw + L.nR; zpR = gw + L.zpR; znR = gw + L.znR; dpR = gw + L.dpR; dnR = gw + L.dnR;
@@ -3129,6 +3148,7 @@ struct Loop {
   long long ld_ps;
   int *st_hist, *it_hist;            // K x B (nullable)
   const int* order;                  // dispatch order: workgroup g runs scenario order[g] (nullable)
+  unsigned long long* times;         // diagnostics (NMPC_STEP_TIMES): K x B x {start, end, XCC_ID|wave<<8}
 };
 
 // One closed-loop step k of scenario b (Python/NMPC_TT.py:348-402 main loop body):
@@ -3136,8 +3156,8 @@ struct Loop {
 // shift_timestep (:13-30).  Everything it reads comes from global memory, so any
 // wavefront can run any (scenario, step) once step k-1 of that scenario is done.
 template <class CAP>
-__device__ __forceinline__ void cl_step(const Params* __restrict__ prm, int B, const IO& io, const Loop& lp,
-                                        const int b, const int k, double* smem) {
+__device__ __forceinline__ int cl_step(const Params* __restrict__ prm, int B, const IO& io, const Loop& lp,
+                                       const int b, const int k, double* smem) {
   // caller layout (external): w = nwE = nuE*N decisions, p = [x0(nxE); xs(3); ...]
   const int nw = prm->nwE, nu = prm->nuE, nx = prm->nxE;
   const double T = prm->T;
@@ -3155,7 +3175,7 @@ __device__ __forceinline__ void cl_step(const Params* __restrict__ prm, int B, c
   ik.f_out = lp.f_hist ? lp.f_hist + kb : nullptr;
   ik.status = lp.st_hist ? lp.st_hist + kb : nullptr;
   ik.iters = lp.it_hist ? lp.it_hist + kb : nullptr;
-  solve_one<CAP>(S, prm, ik, b);
+  const int iters = solve_one<CAP>(S, prm, ik, b);
   sync();
   // shift_timestep: read the solution and the state before anything is overwritten
   const int l = S.lanef();
@@ -3206,6 +3226,7 @@ __device__ __forceinline__ void cl_step(const Params* __restrict__ prm, int B, c
     if (i < nw) wb[i] = wn[j];
   }
   sync();
+  return iters;
 }
 
 // K-step closed loop, one workgroup per scenario running its K steps back to back.
@@ -3217,7 +3238,14 @@ __global__ __launch_bounds__(WAVE, CAP::wpe) void nmpc_closed_loop_kernel(const 
   // the order in which scenarios begin (an out-of-range entry is skipped)
   const int b = lp.order ? lp.order[blockIdx.x] : (int)blockIdx.x;
   if (b < 0 || b >= B) return;
-  for (int k = 0; k < lp.K; ++k) cl_step<CAP>(prm, B, io, lp, b, k, smem);
+  for (int k = 0; k < lp.K; ++k) {
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    cl_step<CAP>(prm, B, io, lp, b, k, smem);
+    if (lp.times && threadIdx.x == 0) {
+      unsigned long long* t = lp.times + ((long long)k * B + b) * 3;
+      t[0] = t0; t[1] = __builtin_amdgcn_s_memrealtime(); t[2] = blockIdx.x;
+    }
+  }
 }
 
 // ---- step-queue scheduler for the K-step closed loop (persistent waves)
@@ -3229,7 +3257,13 @@ __global__ __launch_bounds__(WAVE, CAP::wpe) void nmpc_closed_loop_kernel(const 
 // that has fallen behind (a long chain) is served as soon as its previous step ends,
 // so the launch approaches its longest chain without knowing it in advance.
 //  * Queue (x, j) receives each scenario of XCD set x exactly once, when its step j-1
-//    is done; queue (x, 0) is the dispatch order.  Scenarios are pinned to an XCD
+//    is done; queue (x, 0) is the dispatch order.  Every queue exists twice: a step
+//    whose predecessor took >= hot_iters iterations (max_iter / 2 by default) is
+//    published to the "hot" family, which is served first (lowest step first), then
+//    the normal family (lowest step first).  A scenario that turns locally infeasible
+//    late in its K steps (long steps from then on) would otherwise wait behind the
+//    short steps of scenarios at lower step indices while every wave is busy
+//    (measured: up to 114 ms of a 359 ms launch, scripts/step_times.py).  Scenarios are pinned to an XCD
 //    (set x = dispatch position mod NXCD) and served only by waves running on that XCD
 //    (hardware register XCC_ID): the per-XCD L2s are not coherent with each other, so
 //    a scenario's state (p, w, histories) is only ever handed between waves sharing
@@ -3242,16 +3276,17 @@ __global__ __launch_bounds__(WAVE, CAP::wpe) void nmpc_closed_loop_kernel(const 
 //    short; a wave that waits longer than kSchedWaitTicks anyway sets err and leaves.
 constexpr int NXCD = 8;  // MI355X: 8 XCDs
 struct SchedQ {
-  int* head;  // NXCD x K: claimed count of queue (x, j)
-  int* tail;  // NXCD x K: published count
-  int* resv;  // NXCD x K: reserved count
-  int* ring;  // NXCD x K x BX scenario ids (-1 = not yet written)
+  int* head;  // 2 x NXCD x K: claimed count of queue (family, x, j); family 0 normal, 1 hot
+  int* tail;  // 2 x NXCD x K: published count
+  int* resv;  // 2 x NXCD x K: reserved count
+  int* ring;  // 2 x NXCD x K x BX scenario ids (-1 = not yet written)
   int* err;   // [0]: 1 a wave gave up waiting, 2 a scenario did not complete its K steps;
               // [1]: closed-loop steps completed (nmpc_sched_check_kernel)
   int* done;  // B: steps completed per scenario
   int BX;     // ring capacity per queue = ceil(B / NXCD)
   int one_set;  // test hook (NMPC_SCHED_TEST_ONE_SET): only the waves on XCD 0 run, so
                 // sets 1..7 are never drained and the check must report it
+  int hot_iters;  // a step after one with >= hot_iters iterations goes to the hot family (0: none)
 };
 constexpr unsigned long long kSchedWaitTicks = 1000000000ull;  // s_memrealtime (100 MHz): 10 s
 
@@ -3278,59 +3313,77 @@ __global__ __launch_bounds__(WAVE, CAP::wpe) void nmpc_closed_loop_sched_kernel(
   const int x = xcc_id();
   if (q.one_set && x != 0) return;  // test hook: only XCD 0's waves run (sets 1..7 unserved)
   const int nset = (B - x + NXCD - 1) / NXCD;  // scenarios in this XCD's set
+  // family f = 0 (normal) / 1 (hot) of queue (x, j): counters at [(f * NXCD + x) * K + j]
+  const long long fo = (long long)NXCD * K;
   int* head = q.head + x * K;
   int* tail = q.tail + x * K;
   int* resv = q.resv + x * K;
   int* ring = q.ring + (long long)x * K * q.BX;
+  const long long ro = fo * q.BX;  // ring offset of the hot family
   int jmin = 0;
   for (;;) {
     int cb = -1, ck = -1;
     if (threadIdx.x == 0) {
-      // One pass over the set's queues, lowest step first.  Finding nothing to claim
-      // means every unfinished scenario of the set is running on some wave, so this
-      // wave is surplus from now on (the unfinished count only shrinks, and every
+      // Hot queues first, then normal ones, each lowest step first.  Finding nothing to
+      // claim means every unfinished scenario of the set is running on some wave, so
+      // this wave is surplus from now on (the unfinished count only shrinks, and every
       // publisher claims again right after publishing): it exits instead of spinning.
-      for (int j = jmin; j < K; ++j) {
-        const int h = ld_acq(head + j);
-        if (h >= nset) {
-          if (j == jmin) ++jmin;
-          continue;
+      bool claimed = false;
+      for (int f = 1; f >= 0 && !claimed; --f) {
+        int* hd = head + f * fo;
+        int* tl = tail + f * fo;
+        int* rg = ring + f * ro;
+        for (int j = jmin; j < K; ++j) {
+          const int h = ld_acq(hd + j);
+          if (f == 0 && h + ld_acq(head + fo + j) >= nset) {  // every scenario has passed queue j
+            if (j == jmin) ++jmin;
+            continue;
+          }
+          if (h >= ld_acq(tl + j)) continue;  // nothing published in this queue yet
+          int e = h;
+          if (!__hip_atomic_compare_exchange_strong(hd + j, &e, h + 1, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                    __HIP_MEMORY_SCOPE_AGENT)) {
+            --j;  // lost the race for this queue: look at it again
+            continue;
+          }
+          // published count > h: slot h's writer has reserved it and stores it next
+          const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+          int v = ld_acq(rg + (long long)j * q.BX + h);
+          while (v < 0 && __builtin_amdgcn_s_memrealtime() - t0 < kSchedWaitTicks) {
+            __builtin_amdgcn_s_sleep(2);
+            v = ld_acq(rg + (long long)j * q.BX + h);
+          }
+          if (v < 0) __hip_atomic_store(q.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          else { cb = v; ck = j; }
+          claimed = true;
+          break;
         }
-        if (h >= ld_acq(tail + j)) continue;  // nothing published in this queue yet
-        int e = h;
-        if (!__hip_atomic_compare_exchange_strong(head + j, &e, h + 1, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                                  __HIP_MEMORY_SCOPE_AGENT)) {
-          --j;  // lost the race for this queue: look at it again
-          continue;
-        }
-        // published count > h: slot h's writer has reserved it and stores it next
-        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-        int v = ld_acq(ring + (long long)j * q.BX + h);
-        while (v < 0 && __builtin_amdgcn_s_memrealtime() - t0 < kSchedWaitTicks) {
-          __builtin_amdgcn_s_sleep(2);
-          v = ld_acq(ring + (long long)j * q.BX + h);
-        }
-        if (v < 0) __hip_atomic_store(q.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        else { cb = v; ck = j; }
-        break;
       }
     }
     cb = __builtin_amdgcn_readfirstlane(cb);
     ck = __builtin_amdgcn_readfirstlane(ck);
     if (ck < 0) break;
+    int its = 0;
     if (cb >= 0 && cb < B) {  // an out-of-range dispatch entry is claimed and skipped
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // the previous step's p, w (L1 invalidated)
-      cl_step<CAP>(prm, B, io, lp, cb, ck, smem);
+      const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+      its = cl_step<CAP>(prm, B, io, lp, cb, ck, smem);
+      if (lp.times && threadIdx.x == 0) {
+        unsigned long long* t = lp.times + ((long long)ck * B + cb) * 3;
+        t[0] = t0; t[1] = __builtin_amdgcn_s_memrealtime(); t[2] = (unsigned long long)(x | (blockIdx.x << 8));
+      }
       if (threadIdx.x == 0) q.done[cb] = ck + 1;
       stores_done();  // this step's p, w, histories are in the XCD's L2
     }
     if (threadIdx.x == 0 && ck + 1 < K) {
       const int j = ck + 1;
-      const int pos = __hip_atomic_fetch_add(resv + j, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int f = (q.hot_iters > 0 && its >= q.hot_iters) ? 1 : 0;
+      const int pos = __hip_atomic_fetch_add(resv + f * fo + j, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (pos < q.BX) {
-        __hip_atomic_store(ring + (long long)j * q.BX + pos, cb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(ring + f * ro + (long long)j * q.BX + pos, cb, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
         stores_done();
-        __hip_atomic_fetch_add(tail + j, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_add(tail + f * fo + j, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     }
   }
@@ -3340,8 +3393,12 @@ __global__ __launch_bounds__(WAVE, CAP::wpe) void nmpc_closed_loop_sched_kernel(
 // queue (x, 0) = the set-x entries of the dispatch order (identity or the caller's
 // permutation); every other queue empty
 __global__ void nmpc_sched_init_kernel(int B, int K, const int* order, SchedQ q) {
-  const long long n = (long long)NXCD * K * q.BX;
+  const long long n = (long long)NXCD * K * q.BX;  // one family's ring
   const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) q.ring[n + i] = -1;  // hot family: empty
+  if (i < (long long)NXCD * K) {  // hot family counters
+    q.head[NXCD * K + i] = 0; q.tail[NXCD * K + i] = 0; q.resv[NXCD * K + i] = 0;
+  }
   if (i < n) {
     const int x = (int)(i / ((long long)K * q.BX));
     const long long r = i - (long long)x * K * q.BX;
@@ -3483,6 +3540,8 @@ struct nmpc_handle {
   int last_waves = 0;          // workgroups launched by the last closed-loop launch
   long long last_steps = 0;    // B*K of the last closed-loop launch
   int* last_err = nullptr;     // device flags of the last step-queue launch (SchedQ::err)
+  unsigned long long* dtimes = nullptr;  // diagnostics: step timestamps of the last closed loop
+  size_t times_bytes = 0, times_n = 0;
   int ws_doubles = 0;
   bool trace = false;
   double* dtrace = nullptr;
@@ -3540,6 +3599,14 @@ void nmpc_default_options(nmpc_options* o) {
 }
 
 const char* nmpc_last_error(void) { return g_err.c_str(); }
+
+int nmpc_closed_loop_times(nmpc_handle* h, uint64_t* host_out, int64_t n) {
+  if (!h || !host_out) return fail(NMPC_E_INVALID, "null argument");
+  if (!h->dtimes || (size_t)n < h->times_n) return fail(NMPC_E_INVALID, "no step times recorded (NMPC_STEP_TIMES)");
+  if (hipMemcpy(host_out, h->dtimes, h->times_n * sizeof(uint64_t), hipMemcpyDeviceToHost) != hipSuccess)
+    return fail(NMPC_E_HIP, "reading step times");
+  return NMPC_OK;
+}
 
 #ifndef NMPC_SRC_HASH
 #define NMPC_SRC_HASH "unknown-unknown-unknown-unknown!"
@@ -3646,6 +3713,7 @@ int nmpc_destroy(nmpc_handle* h) {
   if (h->dtrace) hipFree(h->dtrace);
   if (h->dws) hipFree(h->dws);
   if (h->dsched) hipFree(h->dsched);
+  if (h->dtimes) hipFree(h->dtimes);
   delete h;
   return NMPC_OK;
 }
@@ -3839,6 +3907,18 @@ int nmpc_closed_loop_dev(nmpc_handle* h, int32_t B, int32_t K, const double* lbx
   lp.pstep = p_step; lp.ld_ps = ld_ps;
   lp.st_hist = status_hist; lp.it_hist = iters_hist;
   lp.order = order;
+  lp.times = nullptr;
+  if (std::getenv("NMPC_STEP_TIMES")) {  // diagnostics: per-(step, scenario) realtime stamps (100 MHz)
+    const size_t need = (size_t)K * B * 3 * sizeof(unsigned long long);
+    if (need > h->times_bytes) {
+      if (h->dtimes) hipFree(h->dtimes);
+      h->dtimes = nullptr; h->times_bytes = 0;
+      if (hipMalloc(&h->dtimes, need) != hipSuccess) return fail(NMPC_E_NOMEM, "hipMalloc step times");
+      h->times_bytes = need;
+    }
+    lp.times = h->dtimes;
+  }
+  h->times_n = lp.times ? (size_t)K * B * 3 : 0;
   // more scenarios than resident waves: the step-queue scheduler (persistent waves,
   // lowest step first), unless NMPC_CLOSED_LOOP=static (diagnostics: one workgroup per
   // scenario in dispatch order)
@@ -3865,7 +3945,7 @@ int nmpc_closed_loop_dev(nmpc_handle* h, int32_t B, int32_t K, const double* lbx
   h->last_steps = (long long)B * K;
   if (use_q) {
     const int BX = (B + NXCD - 1) / NXCD;
-    const size_t nint = (size_t)3 * NXCD * K + (size_t)NXCD * K * BX + 2 + (size_t)B;
+    const size_t nint = (size_t)6 * NXCD * K + (size_t)2 * NXCD * K * BX + 2 + (size_t)B;
     if (nint * sizeof(int) > h->sched_bytes) {
       if (h->dsched) hipFree(h->dsched);
       h->dsched = nullptr; h->sched_bytes = 0;
@@ -3873,8 +3953,11 @@ int nmpc_closed_loop_dev(nmpc_handle* h, int32_t B, int32_t K, const double* lbx
       h->sched_bytes = nint * sizeof(int);
     }
     SchedQ q;
-    q.head = h->dsched; q.tail = q.head + NXCD * K; q.resv = q.tail + NXCD * K;
-    q.ring = q.resv + NXCD * K; q.err = q.ring + (size_t)NXCD * K * BX; q.done = q.err + 2; q.BX = BX;
+    q.head = h->dsched; q.tail = q.head + 2 * NXCD * K; q.resv = q.tail + 2 * NXCD * K;
+    q.ring = q.resv + 2 * NXCD * K; q.err = q.ring + (size_t)2 * NXCD * K * BX; q.done = q.err + 2; q.BX = BX;
+    // hot family threshold: half of max_iter (NMPC_SCHED_HOT overrides; 0 = one family only)
+    q.hot_iters = h->hp.o.max_iter / 2 > 0 ? h->hp.o.max_iter / 2 : 1;
+    if (const char* hv = std::getenv("NMPC_SCHED_HOT")) q.hot_iters = std::atoi(hv);
     const char* one = std::getenv("NMPC_SCHED_TEST_ONE_SET");
     q.one_set = (one && std::atoi(one) != 0) ? 1 : 0;
     const long long n = (long long)NXCD * K * BX;

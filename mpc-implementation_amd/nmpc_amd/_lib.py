@@ -24,7 +24,7 @@ EXPORTS = (
     "nmpc_default_options", "nmpc_create", "nmpc_destroy", "nmpc_dims",
     "nmpc_solve_batch", "nmpc_solve_batch_dev", "nmpc_set_trace", "nmpc_read_trace",
     "nmpc_shift_dev", "nmpc_closed_loop_dev", "nmpc_closed_loop_info", "nmpc_last_error", "nmpc_kernel_info",
-    "nmpc_build_id",
+    "nmpc_build_id", "nmpc_closed_loop_times",
 )
 
 _OPT_INT = ("max_iter", "acceptable_iter", "max_soc", "max_soft_resto_iters",
@@ -101,6 +101,7 @@ def lib():
                                        + [i64, i64] + [vp, i64] + [vp] * 8)
     L.nmpc_last_error.argtypes = []
     L.nmpc_last_error.restype = C.c_char_p
+    L.nmpc_closed_loop_times.argtypes = [vp, C.POINTER(C.c_uint64), i64]
     L.nmpc_build_id.argtypes = []
     L.nmpc_build_id.restype = C.c_char_p
     L.nmpc_kernel_info.argtypes = [vp, i32p, i32p]

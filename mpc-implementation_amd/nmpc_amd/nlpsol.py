@@ -340,6 +340,13 @@ class Solver:
                                  f"{NOT_RUN} in the history)")
         return info
 
+    def closed_loop_times(self, B: int, K: int):
+        """Diagnostics (NMPC_STEP_TIMES set before the launch): (K, B, 3) uint64 --
+        start / end s_memrealtime stamps (100 MHz) of every step and the running wave."""
+        out = np.zeros((K, B, 3), dtype=np.uint64)
+        _lib.check(_lib.lib().nmpc_closed_loop_times(self._h, out.ctypes.data_as(C.POINTER(C.c_uint64)), out.size))
+        return out
+
     def kernel_info(self):
         lds, tps = C.c_int32(), C.c_int32()
         _lib.check(_lib.lib().nmpc_kernel_info(self._h, C.byref(lds), C.byref(tps)))
