@@ -87,73 +87,43 @@ def pmc_summary(kernel, steps, batch, warmup):
     return out
 
 
-def _cpu_worker(args):
-    """The bench's closed loop on the CPU oracle for scenarios rows[i::nproc]: each
-    scenario runs K warm-started MPC steps (solve, then shift_timestep with the GPU
-    line's target controls, Python/NMPC_TT.py:13-30,348-402) until the budget runs out."""
-    i, nproc, layout, N, T, P, lbx, ubx, lbg, ubg, budget_s, model, K = args
-    import warnings
-    from threadpoolctl import threadpool_limits
-
-    threadpool_limits(1)  # one core per worker process
-    warnings.filterwarnings("ignore", category=RuntimeWarning)  # -inf bounds in the initial-point push
-    sys.path.insert(0, ROOT)
-    from oracle import nmpc_oracle as orc
-
-    prob = orc.make_problem(layout, N=N, T=T, model=model)
-    solver = orc.IpoptDense(prob, orc.REFERENCE_OPTS)
-    nx, nu = prob.nx, prob.nu
-    t0 = time.perf_counter()
-    times, iters, stats, recs = [], [], [], []
-    for row in range(i, P.shape[0], nproc):
-        x0, xs, u0 = P[row, :nx].copy(), P[row, nx:nx + 3].copy(), np.zeros(len(lbx))
-        for k in range(K):
-            if time.perf_counter() - t0 >= budget_s:
-                return times, iters, stats, recs
-            t1 = time.perf_counter()
-            r = solver.solve(u0, lbx, ubx, lbg, ubg, np.concatenate([x0, xs, P[row, nx + 3:]]))
-            times.append(time.perf_counter() - t1)
-            iters.append(r["iter"])
-            stats.append(r["status"])
-            recs.append((row, k, r["status"], r["x"][:nu].copy(), r["f"]))
-            x0, u1, xs = orc.shift_timestep(prob, x0, r["x"].reshape(N, nu).T, xs, con_t=(12.0, 0.01))
-            u0 = u1.T.ravel()
-    return times, iters, stats, recs
-
-
 def cpu_baseline(spec_cfg, cfg, P, lbx, ubx, lbg, ubg, K, budget_s=15.0):
-    """Time the CPU oracle (numpy dense IPOPT restatement, oracle/nmpc_oracle.py) on a
-    bounded sample of the bench's own workload: the same scenarios through the same
-    warm-started closed loop (solve + shift), one scenario per worker process at a time
-    (scenarios split across processes).  Must run before this process
-    touches the GPU (the workers are forked)."""
-    import multiprocessing as mp
+    """Time the compiled CPU restatement (oracle/cpu_ipopt.cpp: C++/OpenMP, the same
+    IPOPT restatement with a Riccati Newton step, pinned to the numpy oracle's
+    fixtures by tests/test_cpu_restatement.py) on the bench's own workload: the same
+    scenarios through the same warm-started closed loop (solve + shift, K steps per
+    scenario from w = 0), one scenario per OpenMP thread at a time, until the
+    budget runs out (scenarios split across cores)."""
+    sys.path.insert(0, ROOT)
+    from oracle import cpu_ipopt, nmpc_oracle as orc
 
     try:
         ncpu = len(os.sched_getaffinity(0))
     except AttributeError:
         ncpu = os.cpu_count() or 1
-    nproc = max(1, min(16, ncpu))  # the GPU box's CPU share is 16
-    layout = "race_track_2" if spec_cfg.n_obs == 10 else (None if spec_cfg.n_obs == 0 else "nmpc_tt")
-    sample = P[: nproc * 64]
+    nthr = max(1, min(16, ncpu))  # the GPU box's CPU share is 16
+    layout = None if spec_cfg.n_obs == 0 else ("race_track_2" if spec_cfg.n_obs == 10 else "nmpc_tt")
+    prob = orc.make_problem(layout, N=spec_cfg.N, T=spec_cfg.T, model=spec_cfg.model)
     t0 = time.perf_counter()
-    with mp.get_context("fork").Pool(nproc) as pool:
-        res = pool.map(_cpu_worker, [(i, nproc, layout, spec_cfg.N, spec_cfg.T, sample, lbx, ubx, lbg, ubg,
-                                      budget_s, spec_cfg.model, K) for i in range(nproc)])
+    r = cpu_ipopt.closed_loop(prob, P, K, lbx, ubx, lbg, ubg, orc.REFERENCE_OPTS, vt=12.0, wt=0.01,
+                              budget_s=budget_s, threads=nthr)
     wall = time.perf_counter() - t0
-    times = np.concatenate([np.asarray(r[0], dtype=float) for r in res])
-    iters = np.concatenate([np.asarray(r[1], dtype=float) for r in res])
-    sts = np.concatenate([np.asarray(r[2], dtype=int) for r in res])
-    n = len(times)
-    cpu_baseline.records = [rec for r in res for rec in r[3]]
-    cpu_baseline.sample_rows = sample.shape[0]
-    return {"value": n / wall, "unit": "MPC steps/s", "cores": nproc, "kind": "port",
-            "sample": f"{n} warm-started closed-loop MPC steps (solve + shift, up to {K} per scenario) of "
-                      f"config-{cfg} scenarios by oracle/nmpc_oracle.py (numpy dense single-shooting IPOPT "
-                      f"restatement), {nproc} worker processes x ~{budget_s:.0f}s, wall {wall:.1f}s",
-            "mean_ip_iterations": float(iters.mean()) if n else None,
-            "solve_ms_p50": float(np.percentile(times, 50) * 1e3) if n else None,
-            "solve_ms_p99": float(np.percentile(times, 99) * 1e3) if n else None,
+    done = r["steps"]
+    n = int(done.sum())
+    rows = np.flatnonzero(done > 0)
+    recs = [(int(b), k, int(r["status"][b, k]), r["u0"][b, k].copy(), float(r["f"][b, k]))
+            for b in rows for k in range(int(done[b]))]
+    cpu_baseline.records = recs
+    cpu_baseline.sample_rows = int(rows.max()) + 1 if len(rows) else 0
+    its = np.concatenate([r["iter"][b, :done[b]] for b in rows]) if len(rows) else np.zeros(0)
+    sts = np.concatenate([r["status"][b, :done[b]] for b in rows]) if len(rows) else np.zeros(0, int)
+    return {"value": n / wall, "unit": "MPC steps/s", "cores": nthr, "kind": "port",
+            "sample": f"{n} warm-started closed-loop MPC steps (solve + shift, up to {K} per scenario, "
+                      f"{len(rows)} of the bench's config-{cfg} scenarios) by oracle/cpu_ipopt.cpp (CPU "
+                      f"restatement, not CasADi: C++/OpenMP IPOPT restatement with a Riccati step), "
+                      f"{nthr} threads, budget {budget_s:.0f}s, wall {wall:.1f}s",
+            "mean_ip_iterations": float(its.mean()) if n else None,
+            "iterations_per_s_per_core": float(its.sum() / wall / nthr) if n else None,
             "status_histogram": {int(k): int(v) for k, v in zip(*np.unique(sts, return_counts=True))}}
 
 
@@ -204,7 +174,7 @@ def parity_sample(solver, spec, P, K, records, bnd, dev, tol=1e-6):
             "status_agreement": agree_status / max(1, compared),
             "steps_before_first_divergence": before_div, "chains_identical": chains_same,
             "max_u0_relerr": max_u, "max_f_relerr": max_f, "tol": tol,
-            "reference": "oracle/nmpc_oracle.py (the cpu_baseline leg's own solves)"}
+            "reference": "oracle/cpu_ipopt.cpp (the cpu_baseline leg's own solves; pinned to oracle/nmpc_oracle.py by tests/test_cpu_restatement.py)"}
 
 
 def main():
@@ -221,7 +191,7 @@ def main():
     ap.add_argument("--no-per-step", action="store_true", help="skip the per-step-launch comparison line")
     ap.add_argument("--in-order", action="store_true",
                     help="fused mode: dispatch scenarios in index order (no longest-first order)")
-    ap.add_argument("--cpu-budget", type=float, default=15.0)
+    ap.add_argument("--cpu-budget", type=float, default=20.0)
     args = ap.parse_args()
 
     import torch
@@ -237,7 +207,7 @@ def main():
     spec = config_spec(args.config)
     B, K, W = args.batch, args.steps, args.warmup
     cpu_res = None
-    if world == 1 and not args.no_cpu_baseline:  # forks workers: before the GPU is initialised
+    if world == 1 and not args.no_cpu_baseline:  # OpenMP threads, before the GPU is initialised
         lb = spec.bounds()
         cpu_res = cpu_baseline(spec, args.config, draw_scenarios(spec, B, seed=1000 + args.config), *lb, K,
                                budget_s=args.cpu_budget)

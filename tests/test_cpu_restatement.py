@@ -1,0 +1,147 @@
+"""The compiled CPU restatement (oracle/cpu_ipopt.cpp -> oracle/libnmpc_cpu.so:
+C++/OpenMP, the same IPOPT restatement as oracle/nmpc_oracle.py with a Riccati
+Newton step; SURVEY.md section 7 step 4, section 4 test 3) checked against the
+numpy oracle's committed fixtures.  It is the bench's CPU baseline, so it has to
+solve the same problems the same way: per-step parity on the closed-loop fixtures
+of BASELINE configs 1, 2, 3 and 5 (status, iterations, x and f at the north-star
+1e-6), the chained closed loop of configs 2 and 3, and the 16 restoration cases.
+CPU-only: runs in the not-gpu suite.
+"""
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLD = os.path.join(ROOT, "tests", "golden")
+sys.path.insert(0, GOLD)
+TOL = 1e-6
+
+
+@pytest.fixture(scope="module")
+def cpu():
+    subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle")], check=True)
+    from oracle import cpu_ipopt
+    return cpu_ipopt
+
+
+def _problem(cfg):
+    from nmpc_amd import config_spec
+    from gen_closed_loop import _problem as prob_of
+    return prob_of(config_spec(cfg))
+
+
+def _relerr(a, b):
+    return np.max(np.abs(a - b) / (1.0 + np.abs(b)), axis=-1)
+
+
+def test_library_exports_and_option_names(cpu):
+    from oracle import nmpc_oracle as orc
+    names = cpu.lib().nmpc_cpu_option_names().decode().split(",")
+    assert set(names) == set(orc.IPOPT_DEFAULTS)
+    a = cpu.options_array(orc.REFERENCE_OPTS)
+    assert a[names.index("max_iter")] == 100 and a[names.index("acceptable_tol")] == 1e-8
+    with pytest.raises(KeyError):
+        cpu.options_array({"no_such_option": 1})
+
+
+@pytest.mark.parametrize("name", ["config1", "config2", "config3", "config5"])
+def test_per_step_parity_with_oracle_fixture(cpu, name):
+    from oracle import nmpc_oracle as orc
+    z = np.load(os.path.join(GOLD, f"closed_loop_{name}.npz"))
+    prob = _problem(int(z["cfg"]))
+    lbx, ubx, lbg, ubg = orc.bounds(prob)
+    W = z["w"].reshape(-1, prob.nw)
+    P = z["p"].reshape(-1, prob.np_)
+    r = cpu.solve_batch(prob, W, P, lbx, ubx, lbg, ubg, orc.REFERENCE_OPTS)
+    ost, oit = z["status"].ravel(), z["iter"].ravel()
+    ox, of = z["x"].reshape(-1, prob.nw), z["f"].ravel()
+    same = r["status"] == ost
+    conv = same & np.isin(ost, (0, 1))
+    ok = conv & (_relerr(r["x"], ox) <= TOL) & (np.abs(r["f"] - of) <= TOL * (1 + np.abs(of)))
+    print(f"\n{name}: {len(ost)} solves; status agree {same.mean():.4f}; iterations agree "
+          f"{(r['iter'] == oit).mean():.4f}; converged+agreeing {conv.sum()}, within 1e-6 {ok.sum()}")
+    assert same.mean() >= 0.98
+    assert ok.sum() >= 0.98 * conv.sum()
+    assert (r["iter"] == oit).mean() >= 0.95
+
+
+def test_config5_cold_solves(cpu):
+    from oracle import nmpc_oracle as orc
+    z = np.load(os.path.join(GOLD, "closed_loop_config5.npz"))
+    prob = _problem(5)
+    lbx, ubx, lbg, ubg = orc.bounds(prob)
+    n = len(z["cold_status"])
+    r = cpu.solve_batch(prob, np.zeros((n, prob.nw)), z["P"][:n], lbx, ubx, lbg, ubg, orc.REFERENCE_OPTS)
+    assert (r["status"] == z["cold_status"]).mean() >= 15 / 16
+    conv = (r["status"] == z["cold_status"]) & np.isin(r["status"], (0, 1))
+    assert np.all(_relerr(r["x"][conv], z["cold_x"][conv]) <= TOL)
+
+
+@pytest.mark.parametrize("name", ["config2", "config3", "config5"])
+def test_chained_closed_loop(cpu, name):
+    """nmpc_cpu_closed_loop (solve + shift_timestep + obstacle schedule) from the
+    fixture's start, compared step by step until a chain first disagrees."""
+    from oracle import nmpc_oracle as orc
+    z = np.load(os.path.join(GOLD, f"closed_loop_{name}.npz"))
+    prob = _problem(int(z["cfg"]))
+    B, K = z["status"].shape
+    r = cpu.closed_loop(prob, z["P"], K, *orc.bounds(prob), orc.REFERENCE_OPTS, vt=float(z["vt"]),
+                        wt=float(z["wt"]), p_step=z["p_step"])
+    assert np.all(r["steps"] == K)
+    nu = prob.nu
+    matched, full = 0, 0
+    for b in range(B):
+        chain = True
+        for k in range(K):
+            st = z["status"][b, k]
+            ok = r["status"][b, k] == st
+            if ok and st in (0, 1):
+                ok = (np.max(np.abs(r["u0"][b, k] - z["x"][b, k, :nu]) / (1 + np.abs(z["x"][b, k, :nu]))) <= TOL
+                      and abs(r["f"][b, k] - z["f"][b, k]) <= TOL * (1 + abs(z["f"][b, k])))
+            if not ok:
+                chain = False
+                break
+            matched += 1
+        full += chain
+    print(f"\n{name} chained: {full}/{B} chains identical over {K} steps; {matched}/{B * K} steps before "
+          f"the first divergence")
+    assert matched >= 0.9 * B * K
+    assert full >= 0.75 * B
+
+
+def test_restoration_cases(cpu):
+    """The 16 captured solves that enter the feasibility restoration phase."""
+    from oracle import nmpc_oracle as orc
+    G = np.load(os.path.join(GOLD, "resto_cases.npz"))
+    prob = orc.make_problem("race_track_2", N=20, T=0.2)
+    r = cpu.solve_batch(prob, G["w"], G["p"], *orc.bounds(prob), orc.REFERENCE_OPTS)
+    agree = int((r["status"] == G["status"]).sum())
+    print(f"\nrestoration cases: final status agrees with the oracle on {agree}/16, iterations on "
+          f"{int((r['iter'] == G['iter']).sum())}/16")
+    assert agree >= 15
+
+
+def test_closed_loop_budget_stops_cleanly(cpu):
+    from oracle import nmpc_oracle as orc
+    prob = _problem(3)
+    z = np.load(os.path.join(GOLD, "closed_loop_config3.npz"))
+    r = cpu.closed_loop(prob, z["P"][:4], 3, *orc.bounds(prob), orc.REFERENCE_OPTS, budget_s=1e-9, threads=2)
+    assert np.all(r["steps"] <= 1)
+    for b in range(4):
+        assert np.all(r["status"][b, r["steps"][b]:] == -1000)
+
+
+def test_equality_rows_rejected_like_the_oracle(cpu):
+    from oracle import nmpc_oracle as orc
+    prob = orc.make_problem(None, N=4, T=0.2)
+    lbx, ubx, lbg, ubg = orc.bounds(prob)
+    lbg, ubg = lbg.copy(), ubg.copy()
+    lbg[2] = ubg[2] = 0.0
+    p = np.array([0, 0, 100, 0, 0, 0, 0, 0, 50, 50, 0.0])
+    r = cpu.solve_batch(prob, np.zeros((1, prob.nw)), p[None], lbx, ubx, lbg, ubg, orc.REFERENCE_OPTS)
+    assert r["status"][0] == -11
+    with pytest.raises(ValueError):
+        orc.IpoptDense(prob, orc.REFERENCE_OPTS).solve(np.zeros(prob.nw), lbx, ubx, lbg, ubg, p)
