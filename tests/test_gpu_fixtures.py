@@ -137,3 +137,57 @@ def test_chained_closed_loop_matches_oracle_fixture(name):
     # steps (the per-step test above compares every step from identical inputs)
     assert matched >= 0.9 * total
     assert full >= 0.75 * B
+
+
+def test_config3_closed_loop_at_bench_scale_matches_cpu_restatement():
+    """The bench's own workload (BASELINE config 3: 4096 scenarios, seed 1003, 20
+    warm-started closed-loop MPC steps from u = 0, target controls (12, 0.01)) through
+    nmpc_closed_loop_dev and through the compiled CPU restatement
+    (oracle/cpu_ipopt.cpp, pinned to the numpy oracle by tests/test_cpu_restatement.py),
+    compared step by step until each chain first disagrees: status, and u0 / f within
+    the north-star 1e-6 (1 + |ref|) for converged steps."""
+    import sys
+    import torch
+    from nmpc_amd import config_spec, draw_scenarios
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    from oracle import cpu_ipopt, nmpc_oracle as orc
+
+    spec, s = _solver(3)
+    B, K = 4096, 20
+    P = draw_scenarios(spec, B, seed=1003)
+    prob = orc.make_problem("race_track_2", N=spec.N, T=spec.T)
+    ref = cpu_ipopt.closed_loop(prob, P, K, *orc.bounds(prob), orc.REFERENCE_OPTS, vt=12.0, wt=0.01, threads=16)
+    assert np.all(ref["steps"] == K)
+    f64 = dict(dtype=torch.float64, device="cuda")
+    bnd = [torch.tensor(v, **f64) for v in spec.bounds()]
+    hist = {"u": torch.empty(K, B, 6, **f64), "f": torch.empty(K, B, **f64),
+            "status": torch.empty(K, B, dtype=torch.int32, device="cuda")}
+    s.closed_loop_device(K, *bnd, torch.tensor(P, **f64), torch.zeros(B, spec.nw, **f64),
+                         torch.full((B,), 12.0, **f64), torch.full((B,), 0.01, **f64), hist)
+    torch.cuda.synchronize()
+    H = {k: v.cpu().numpy() for k, v in hist.items()}
+    gs, rs = H["status"].T, ref["status"]
+    agree = (gs == rs).mean()
+    matched, full, worst = 0, 0, 0.0
+    for b in range(B):
+        chain = True
+        for k in range(K):
+            ok = gs[b, k] == rs[b, k]
+            if ok and rs[b, k] in (0, 1):
+                eu = np.max(np.abs(H["u"][k, b] - ref["u0"][b, k]) / (1 + np.abs(ref["u0"][b, k])))
+                ef = abs(H["f"][k, b] - ref["f"][b, k]) / (1 + abs(ref["f"][b, k]))
+                ok = eu <= TOL and ef <= TOL
+                if ok:
+                    worst = max(worst, eu, ef)
+            if not ok:
+                chain = False
+                break
+            matched += 1
+        full += chain
+    print(f"\nconfig 3 at bench scale: status agreement {agree:.4f} over {B * K} steps; {full}/{B} chains "
+          f"identical; {matched} steps before the first divergence; max rel err {worst:.2e}")
+    assert agree >= 0.99
+    assert full >= 0.9 * B
+    assert matched >= 0.95 * B * K
