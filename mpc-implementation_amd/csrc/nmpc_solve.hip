@@ -3560,6 +3560,11 @@ static void pick_class(const Params& P, KernFn* fn, LoopFn* lfn, SchedFn* sfn, i
   else if (fit_a) c = nmpc_class_fns_A();
   else if (P.N <= CapB::nmax && P.m <= CapB::mmax) c = nmpc_class_fns_B();
   else c = nmpc_class_fns_C();
+  // diagnostics: run a fitting problem on a larger class (global row vectors)
+  if (const char* e = std::getenv("NMPC_FORCE_CLASS")) {
+    if (e[0] == 'B' && P.N <= CapB::nmax && P.m <= CapB::mmax && !P.o.linear_solver_fp32) c = nmpc_class_fns_B();
+    if (e[0] == 'C' && !P.o.linear_solver_fp32) c = nmpc_class_fns_C();
+  }
   *fn = c.fn; *lfn = c.lfn; *sfn = c.sfn; *lds_doubles = c.lds_doubles; *ws_doubles = c.ws_doubles;
 }
 
