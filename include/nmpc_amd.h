@@ -134,7 +134,11 @@ int nmpc_dims(const nmpc_handle* h, int32_t* nw, int32_t* ng, int32_t* np, int32
 
 /* Replaces sol = solver(x0=, lbx=, ubx=, lbg=, ubg=, p=) (Python/NMPC_TT.py:358-365)
  * for B scenarios at once.  HOST pointers; synchronous.  Output pointers other
- * than x_out may be NULL. */
+ * than x_out may be NULL.
+ * Bounds as IPOPT reads them: |b| >= 1e19 is no bound; lbx == ubx fixes a variable
+ * (fixed_variable_treatment = make_parameter: held at the bound, no step, lam_x 0);
+ * lbx > ubx and equality rows lbg == ubg report status -11 (IPOPT Invalid_Problem_Definition)
+ * for that scenario. */
 int nmpc_solve_batch(nmpc_handle* h, int32_t B,
                      const double* x0, int64_t ld_x0,
                      const double* lbx, int64_t ld_lbx, const double* ubx, int64_t ld_ubx,

@@ -84,6 +84,7 @@ struct Lay {
   int trig, qs, lam;
   int kf, Rc, P0, P1, pv0, pv1, St;
   int p, ob, inc, red, rvars, rdX;
+  int fixm;     // per-stage bit mask of fixed controls (ints)
   int total;    // LDS doubles per scenario
   int wstotal;  // global-workspace doubles per scenario
 };
@@ -140,7 +141,8 @@ constexpr Lay make_layout(int N, int m, bool lr, bool refine) {
   L.red = o;
 #endif
   L.dl = o; o += al2(ng); L.du = o; o += al2(ng);  // row bounds (constant during a solve, read by every row pass)
-  L.rvars = o; o += 48;  // line-search / restoration scalars; [32..36] barrier sums; [40..45] watchdog
+  L.rvars = o; o += 48;  // line-search / restoration scalars; [32..36] barrier sums; [40..45] watchdog; [46] #fixed
+  L.fixm = o; o += al2(N / 2 + 1);  // fixed-control masks, one int per stage
   L.rdX = o; if (refine) o += al2(nX);  // refinement step in X (fp32 classes)
   if (lr) {
     L.s = o; o += al2(ng); L.y = o; o += al2(ng); L.vl = o; o += al2(ng); L.vu = o; o += al2(ng);
@@ -364,10 +366,15 @@ struct Solver {
   LDS double* kf, *Rc, *Pa, *Pb, *pva, *pvb, *St;
   LDS double* pp, *obx, *oby, *inc, *stamps;
   GLB double* filt;
+  LDS int* fixm;  // fixed decision variables (lbx == ubx, make_parameter): bit c of stage k
   // uniform scalars
   double df, mu, tau, delta;
   int nfilt;
   int nzx, nzs;
+  int nfix;  // number of fixed decision variables (0: none, the common case)
+  __device__ __forceinline__ bool fixed(int i) const {  // decision i = 6k + c (internal layout)
+    return nfix > 0 && ((fixm[i / 6] >> (i - 6 * (i / 6))) & 1);
+  }
 
   __device__ __forceinline__ void bind(const Params* prm, double* smem, double* wsp, int lane_, int b_) {
     constexpr Lay L = CAP::L;
@@ -405,6 +412,8 @@ struct Solver {
     pp = sm + L.p; obx = sm + L.ob; oby = obx + NMPC_MAX_OBS; inc = sm + L.inc;
     filt = gw + L.filt;
     stamps = sm + L.red;
+    fixm = (LDS int*)(sm + L.fixm);
+    nfix = 0;
   }
 
   __device__ __forceinline__ bool hasl(double v) const { return v > -INFINITY; }
@@ -955,6 +964,8 @@ struct Solver {
       const R E03 = (R)E03d, E04 = (R)E04d, E13 = (R)E13d, E14 = (R)E14d, E23 = (R)E23d;
       const R b00 = (R)b00d, b10 = (R)b10d, b20 = (R)b20d;
       const R zr = (R)0;
+      // fixed controls (make_parameter) leave the stage problem: unit pivot, no coupling
+      const int fm = nfix > 0 ? fixm[k] : 0;
       const R aj0 = (j == 3) ? E03 : (j == 4 ? E04 : zr);
       const R aj1 = (j == 3) ? E13 : (j == 4 ? E14 : zr);
       const R aj2 = (j == 3) ? E23 : zr;
@@ -976,6 +987,7 @@ struct Solver {
         const R PArj = Prj + ((Pr0 * aj0 + Pr1 * aj1) + Pr2 * aj2);
         R stv = (i == 0) ? ((b00 * PA0j + b10 * PA1j) + b20 * PA2j) : Tr * PArj;
         stv += (i == 0 && j == 3) ? (R)qs[k * 10 + 8] : ((i == 0 && j == 4) ? (R)qs[k * 10 + 9] : zr);
+        if ((fm >> i) & 1) stv = zr;
         if (ln < 48) Stc[ln] = stv;
         if (tR >= 0) {
           R v;
@@ -990,6 +1002,7 @@ struct Solver {
           }
           // an absent control (model embedding) keeps a unit pivot: zero step, no inertia effect
           if (rR == cR) v = (rR >= nuE) ? (R)1 : v + (rdk + dlt);
+          if (((fm >> rR) | (fm >> cR)) & 1) v = (rR == cR) ? (R)1 : zr;
           Rcc[tR] = v;
           Rk[k * 21 + tR] = (double)v;
         }
@@ -1021,6 +1034,9 @@ struct Solver {
         rt[0] = readlane_d(rvk, 0) + ((b00 * pc[0] + b10 * pc[1]) + b20 * pc[2]);
 #pragma unroll
         for (int r = 1; r < 6; ++r) rt[r] = readlane_d(rvk, r) + Tr * pc[2 + r];
+#pragma unroll
+        for (int r = 0; r < 6; ++r)
+          if ((fm >> r) & 1) rt[r] = zr;
         R ya[6], yb[6];
 #pragma unroll
         for (int r = 0; r < 6; ++r) {
@@ -1115,6 +1131,12 @@ struct Solver {
       rt[0] = (R)rv[k * 6 + 0] + ((b00 * p8[0] + b10 * p8[1]) + b20 * p8[2]);
 #pragma unroll
       for (int r = 1; r < 6; ++r) rt[r] = (R)rv[k * 6 + r] + Tr * p8[2 + r];
+      if (nfix > 0) {
+        const int fm = fixm[k];
+#pragma unroll
+        for (int r = 0; r < 6; ++r)
+          if ((fm >> r) & 1) rt[r] = (R)0;
+      }
 #pragma unroll
       for (int r = 0; r < 6; ++r) {
         R a = rt[r];
@@ -1216,7 +1238,7 @@ struct Solver {
           double r = rv[k * 6 + c] + (Rd[k * 6 + c] + delta) * dUo[k * 6 + c];
           r += (c == 0) ? ((b00 * ln[0] + b10 * ln[1]) + b20 * ln[2]) + (qs[k * 10 + 8] * dxk[3] + qs[k * 10 + 9] * dxk[4])
                         : T * ln[2 + c];
-          rres[k * 6 + c] = (c < nuE) ? r : 0.0;  // absent controls: unit pivot, zero step
+          rres[k * 6 + c] = (c < nuE && !fixed(k * 6 + c)) ? r : 0.0;  // absent / fixed: zero step
         }
       }
       sync();
@@ -1676,6 +1698,7 @@ __device__ __forceinline__ void resto_phase(const Params* __restrict__ prm, doub
   extern __shared__ __attribute__((aligned(16))) double smem[];
   Solver<CAP> S;
   S.bind(prm, smem, ws, threadIdx.x, b);
+  S.nfix = (int)S.rvars[46];
   S.df = io.df; S.nfilt = io.nfilt; S.nzx = io.nzx; S.nzs = io.nzs; S.delta = 0.0;
   S.mu = io.mu0; S.tau = io.tau0;
   const nmpc_options& o = prm->o;
@@ -1816,7 +1839,7 @@ __device__ __forceinline__ void resto_phase(const Params* __restrict__ prm, doub
         bool bad = false;
         for (int i = S.lanef(); i < nw; i += WAVE) {
           const double dd = S.U[i] - S.UR[i];
-          const double g = S.grad_u(i) + S.etaR * S.dr2(i) * dd - S.zl[i] + S.zu[i];
+          const double g = S.fixed(i) ? 0.0 : S.grad_u(i) + S.etaR * S.dr2(i) * dd - S.zl[i] + S.zu[i];
           if (!isfinite(g)) bad = true;
           dinf = fmax(dinf, fabs(g));
           if (S.hasl(S.xl[i])) cmr = fmax(cmr, fabs((S.U[i] - S.xl[i]) * S.zl[i]));
@@ -1885,7 +1908,8 @@ __device__ __forceinline__ void resto_phase(const Params* __restrict__ prm, doub
             const double et = o.resto_proximity_weight * sqrt(mu_);
             double dn = 0.0, cm = 0.0, pinf = 0.0;
             for (int i = S.lanef(); i < nw; i += WAVE) {
-              const double g = S.grad_u(i) + et * S.dr2(i) * (S.U[i] - S.UR[i]) - S.zl[i] + S.zu[i];
+              const double g =
+                  S.fixed(i) ? 0.0 : S.grad_u(i) + et * S.dr2(i) * (S.U[i] - S.UR[i]) - S.zl[i] + S.zu[i];
               dn = fmax(dn, fabs(g));
               if (S.hasl(S.xl[i])) cm = fmax(cm, fabs((S.U[i] - S.xl[i]) * S.zl[i] - mu_));
               if (S.hasu(S.xu[i])) cm = fmax(cm, fabs((S.xu[i] - S.U[i]) * S.zu[i] - mu_));
@@ -2287,6 +2311,9 @@ __device__ __forceinline__ int solve_one(Solver<CAP>& S, const Params* __restric
   }
   const double brf = o.bound_relax_factor, cvt = o.constr_viol_tol;
   bool invalid = false;
+  if (S.lanef() <= N) S.fixm[S.lanef()] = 0;
+  sync();
+  double nfix_l = 0.0;
   for (int i = S.lanef(); i < nw; i += WAVE) {
     const int e = ext_u(prm, i);  // external decision index, -1: absent control (fixed at 0, unbounded)
     S.U[i] = e >= 0 ? io.x0[(long long)b * io.ld_x0 + e] : 0.0;
@@ -2295,7 +2322,14 @@ __device__ __forceinline__ int solve_one(Solver<CAP>& S, const Params* __restric
     S.xl[i] = lo > -BIGB ? lo - fmin(cvt, brf * fmax(1.0, fabs(lo))) : -INFINITY;
     S.xu[i] = hi < BIGB ? hi + fmin(cvt, brf * fmax(1.0, fabs(hi))) : INFINITY;
     if (lo > hi) invalid = true;
+    if (lo > -BIGB && lo == hi) {  // fixed variable (IPOPT make_parameter): held at the bound, unbounded
+      S.U[i] = lo; S.xl[i] = -INFINITY; S.xu[i] = INFINITY;
+      atomicOr((int*)&S.fixm[i / 6], 1 << (i - 6 * (i / 6)));
+      nfix_l += 1.0;
+    }
   }
+  S.nfix = (int)wsum(nfix_l);
+  if (S.lanef() == 0) S.rvars[46] = (double)S.nfix;
   for (int r = S.lanef(); r < ng; r += WAVE) {
     const double lo = io.lbg[(long long)b * io.ld_lbg + r], hi = io.ubg[(long long)b * io.ld_ubg + r];
     S.dl[r] = lo > -BIGB ? lo - fmin(cvt, brf * fmax(1.0, fabs(lo))) : -INFINITY;  // unscaled for now
@@ -2323,7 +2357,7 @@ __device__ __forceinline__ int solve_one(Solver<CAP>& S, const Params* __restric
     double gmax = 0.0;
     bool bad = !isfinite(F0);
     for (int i = S.lanef(); i < nw; i += WAVE) {
-      const double g = S.grad_u(i);
+      const double g = S.fixed(i) ? 0.0 : S.grad_u(i);  // fixed variables leave the scaling
       if (!isfinite(g)) bad = true;
       gmax = fmax(gmax, fabs(g));
     }
@@ -2353,19 +2387,22 @@ __device__ __forceinline__ int solve_one(Solver<CAP>& S, const Params* __restric
         for (int j = k - 1; j >= 0; --j) {
           double E03, E04, E13, E14, E23, b00, b10, b20;
           S.stage_AB(j, E03, E04, E13, E14, E23, b00, b10, b20);
+          // column of control c of stage j (fixed controls are no columns: make_parameter)
+          const int fmj = S.nfix > 0 ? S.fixm[j] : 0;
+          auto col = [&](int c, double v) { return ((fmj >> c) & 1) ? 0.0 : fabs(v); };
           // rows z, theta, x5, x6, x7
-          rmax[0] = fmax(rmax[0], fmax(fabs(b20), fabs(T * e23)));
-          rmax[1] = fmax(rmax[1], fabs(T));
+          rmax[0] = fmax(rmax[0], fmax(col(0, b20), col(1, T * e23)));
+          rmax[1] = fmax(rmax[1], col(1, T));
           if (nb == 5) {  // gimbal rows x5, x6, x7
-            rmax[2] = fmax(rmax[2], fabs(T));
-            rmax[3] = fmax(rmax[3], fabs(T));
-            rmax[4] = fmax(rmax[4], fabs(T));
+            rmax[2] = fmax(rmax[2], col(3, T));
+            rmax[3] = fmax(rmax[3], col(4, T));
+            rmax[4] = fmax(rmax[4], col(5, T));
           }
           for (int q = 0; q < S.nobs; ++q) {
             const double jv = gxo[q] * b00 + gyo[q] * b10;
             const double jt = T * (gxo[q] * e03 + gyo[q] * e13);
             const double jp = T * (gxo[q] * e04 + gyo[q] * e14);
-            rmax[nb + q] = fmax(rmax[nb + q], fmax(fabs(jv), fmax(fabs(jt), fabs(jp))));
+            rmax[nb + q] = fmax(rmax[nb + q], fmax(col(0, jv), fmax(col(1, jt), col(2, jp))));
           }
           e03 += E03; e04 += E04; e13 += E13; e14 += E14; e23 += E23;
         }
@@ -2500,7 +2537,7 @@ __device__ __forceinline__ int solve_one(Solver<CAP>& S, const Params* __restric
     const double muc = S.mu;
     bool bad = false;
     for (int i = S.lanef(); i < nw; i += WAVE) {
-      const double g = S.grad_u(i) - S.zl[i] + S.zu[i];
+      const double g = S.fixed(i) ? 0.0 : S.grad_u(i) - S.zl[i] + S.zu[i];
       if (!isfinite(g)) bad = true;
       dinf = fmax(dinf, fabs(g));
       if (S.hasl(S.xl[i])) cmp = fmax(cmp, fabs((S.U[i] - S.xl[i]) * S.zl[i]));
@@ -2747,7 +2784,7 @@ __device__ __forceinline__ int solve_one(Solver<CAP>& S, const Params* __restric
       // current pd error (grad_lag from the adjoint computed at loop start)
       double dual = 0, prim = 0, cm = 0;
       for (int i = S.lanef(); i < nw; i += WAVE) {
-        dual += fabs(S.grad_u(i) - S.zl[i] + S.zu[i]);
+        dual += S.fixed(i) ? 0.0 : fabs(S.grad_u(i) - S.zl[i] + S.zu[i]);
         if (S.hasl(S.xl[i])) cm += fabs((S.U[i] - S.xl[i]) * S.zl[i] - mu);
         if (S.hasu(S.xu[i])) cm += fabs((S.xu[i] - S.U[i]) * S.zu[i] - mu);
       }
@@ -2757,7 +2794,7 @@ __device__ __forceinline__ int solve_one(Solver<CAP>& S, const Params* __restric
         if (S.hasl(S.dl[r])) cm += fabs((S.s[r] - S.dl[r]) * S.vl[r] - mu);
         if (S.hasu(S.du[r])) cm += fabs((S.du[r] - S.s[r]) * S.vu[r] - mu);
       }
-      const double nn = (double)(S.nwE + ng);
+      const double nn = (double)(S.nwE - S.nfix + ng);
       const double e_c = wsum(dual) / nn + (ng ? wsum(prim) / ng : 0.0) + (nc ? wsum(cm) / nc : 0.0);
       double ft, phit, tht;
       ++ls_trials;
@@ -2782,7 +2819,7 @@ __device__ __forceinline__ int solve_one(Solver<CAP>& S, const Params* __restric
         double dzl, dzu;
         S.dz_x(i, S.dU[i], dzl, dzu);
         const double zlt = S.zl[i] + a * dzl, zut = S.zu[i] + a * dzu;
-        dual2 += fabs(S.grad_u(i) - zlt + zut);
+        dual2 += S.fixed(i) ? 0.0 : fabs(S.grad_u(i) - zlt + zut);
         if (S.hasl(S.xl[i])) cm2 += fabs((S.Ut[i] - S.xl[i]) * zlt - mu);
         if (S.hasu(S.xu[i])) cm2 += fabs((S.xu[i] - S.Ut[i]) * zut - mu);
       }

@@ -68,6 +68,8 @@ def make_options(opts: dict | None) -> _lib.Options:
                 raise ValueError("only mu_strategy='monotone' (IPOPT default) is supported")
             if name == "nlp_scaling_method" and v != "gradient-based":
                 raise ValueError("only nlp_scaling_method='gradient-based' (IPOPT default) is supported")
+            if name == "fixed_variable_treatment" and v != "make_parameter":
+                raise ValueError("only fixed_variable_treatment='make_parameter' (IPOPT default) is supported")
             continue  # output / linear-solver choices do not change the iterates here
         if not hasattr(o, name):
             raise ValueError(f"unsupported IPOPT option {k!r}")

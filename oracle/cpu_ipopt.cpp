@@ -452,6 +452,7 @@ void add_rows(const Prob& P, const Ev& ev, const double* wr, const double* dc, d
 struct Riccati {
   int N = 0, nx = 0, nu = 0;
   Vec K, L, idg, kv;
+  const char* fix = nullptr;  // fixed decision variables (make_parameter): decoupled, zero step
   void size(const Prob& p) {
     N = p.N; nx = p.nx; nu = p.nu;
     K.assign(N * 48, 0.0);
@@ -547,6 +548,13 @@ struct Riccati {
       if (k > 0)
         for (int a = 0; a < NU; ++a)
           for (int j = 0; j < NX; ++j) St[a * 8 + j] += S[k * 48 + a * 8 + j];
+      if (fix)  // a fixed control leaves the problem: unit pivot, no coupling
+        for (int a = 0; a < NU; ++a)
+          if (fix[k * NU + a]) {
+            for (int c = 0; c < NU; ++c) Rt[a * 6 + c] = Rt[c * 6 + a] = 0.0;
+            Rt[a * 6 + a] = 1.0;
+            for (int j = 0; j < NX; ++j) St[a * 8 + j] = 0.0;
+          }
       double* Lk = L.data() + k * 36;
       double* ik = idg.data() + k * 6;
       if (!chol_t<NU>(Rt, Lk, ik)) return false;
@@ -585,6 +593,7 @@ struct Riccati {
       BT_mul(ab, p, rt);
       for (int a = 0; a < NU; ++a) {
         rt[a] += r[k * NU + a];
+        if (fix && fix[k * NU + a]) rt[a] = 0.0;
         v[a] = rt[a];
       }
       chol_solve_t<NU>(L.data() + k * 36, idg.data() + k * 6, v);
@@ -696,7 +705,8 @@ class Solver {
   Riccati ric;
   Vec Qb, Qw, Sb, qv, dXs;
   // bounds
-  Mask xlm, xum, slm, sum_;
+  Mask xlm, xum, slm, sum_, fixd;
+  int nf = 0;  // free decision variables (n minus the fixed ones)
   Vec xl, xu, dl, du, gl_, gu_, dampxl, dampxu, dampsl, dampsu, dc;
   double df = 1.0;
   int nzx = 0, nzs = 0;
@@ -761,7 +771,7 @@ class Solver {
                 Vec& gls) const {
     glx.assign(n, 0.0);
     adjoint(P_, ev, df, y.data(), dc.data(), glx.data());
-    for (int i = 0; i < n; ++i) glx[i] = glx[i] - zl[i] + zu[i];
+    for (int i = 0; i < n; ++i) glx[i] = fixd[i] ? 0.0 : glx[i] - zl[i] + zu[i];
     gls.resize(m);
     for (int r = 0; r < m; ++r) gls[r] = -y[r] - vl[r] + vu[r];
   }
@@ -878,16 +888,26 @@ void Solver::solve(const double* w0p, const double* p, const double* lbxp, const
     C.ox[j] = P_.oxp[j] >= 0 ? p[P_.oxp[j]] : P_.ox[j];
     C.oy[j] = P_.oyp[j] >= 0 ? p[P_.oyp[j]] : P_.oy[j];
   }
-  const Vec w0(w0p, w0p + n);
+  const Vec w0in(w0p, w0p + n);
   R.x.assign(n, 0.0); R.g.assign(m, 0.0); R.lam_x.assign(n, 0.0); R.lam_g.assign(m, 0.0);
   for (int r = 0; r < m; ++r) {
     if (std::fabs(lbgp[r]) < INF && lbgp[r] == ubgp[r]) {  // equality rows: not restated (oracle raises)
-      R.status = ST_EQ; R.iter = 0; R.x = w0;
+      R.status = ST_EQ; R.iter = 0; R.x = w0in;
       return;
     }
   }
-  xlm.assign(n, 0); xum.assign(n, 0); slm.assign(m, 0); sum_.assign(m, 0);
-  for (int i = 0; i < n; ++i) { xlm[i] = lbxp[i] > -INF; xum[i] = ubxp[i] < INF; }
+  xlm.assign(n, 0); xum.assign(n, 0); slm.assign(m, 0); sum_.assign(m, 0); fixd.assign(n, 0);
+  // fixed variables (lbx == ubx): IPOPT's default make_parameter -- held at the bound,
+  // no bounds / multipliers / step, out of the scaling maxima and error norms (oracle)
+  Vec w0 = w0in;
+  nf = n;
+  for (int i = 0; i < n; ++i) {
+    fixd[i] = std::fabs(lbxp[i]) < INF && lbxp[i] == ubxp[i];
+    if (fixd[i]) { w0[i] = lbxp[i]; --nf; }
+    xlm[i] = lbxp[i] > -INF && !fixd[i];
+    xum[i] = ubxp[i] < INF && !fixd[i];
+  }
+  ric.fix = fixd.data();
   for (int r = 0; r < m; ++r) { slm[r] = lbgp[r] > -INF; sum_[r] = ubgp[r] < INF; }
   xl = relax(lbxp, n, -1.0); xu = relax(ubxp, n, +1.0);
   gl_ = relax(lbgp, m, -1.0); gu_ = relax(ubgp, m, +1.0);
@@ -937,6 +957,7 @@ void Solver::solve(const double* w0p, const double* p, const double* lbxp, const
       for (int i = 0; i < P_.mr; ++i) {
         double mx = 0.0;
         for (int c = 0; c < n; ++c) {
+          if (fixd[c]) continue;
           double v;
           if (i < P_.nb) {
             v = Zk[P_.bs[i] * n + c];
@@ -953,12 +974,17 @@ void Solver::solve(const double* w0p, const double* p, const double* lbxp, const
   }
   dc.assign(m, 1.0);
   df = 1.0;
-  if (!(allfinite(gradF) && jfin)) {
+  bool gfin = true;
+  for (int i = 0; i < n; ++i)
+    if (!fixd[i] && !std::isfinite(gradF[i])) gfin = false;
+  if (!(gfin && jfin)) {
     Vec zz(n, 0.0), zm(m, 0.0);
     finish(w0, 0, ST_INVALID, zz, zz, zm);
     return;
   }
-  const double gmax = n ? amax(gradF) : 0.0;
+  double gmax = 0.0;
+  for (int i = 0; i < n; ++i)
+    if (!fixd[i]) gmax = std::max(gmax, std::fabs(gradF[i]));
   if (gmax > o.nlp_scaling_max_gradient) df = o.nlp_scaling_max_gradient / gmax;
   df = std::max(df, o.nlp_scaling_min_value);
   double rmx = 0.0;
@@ -1054,7 +1080,7 @@ void Solver::solve(const double* w0p, const double* p, const double* lbxp, const
                       const Vec& zu_, const Vec& vl_, const Vec& vu_, double mu_) {
     Vec gx, gs;
     grad_lag(ev_, y_, zl_, zu_, vl_, vu_, gx, gs);
-    const double dual = (sumabs(gx) + sumabs(gs)) / (n + m);
+    const double dual = (sumabs(gx) + sumabs(gs)) / (nf + m);
     double prim = 0.0;
     for (int r = 0; r < m; ++r) prim += std::fabs(d_[r] - s_[r]);
     prim = m ? prim / m : 0.0;
@@ -1552,7 +1578,8 @@ void Solver::restoration(const Vec& x0, const Vec& s0, const Vec& d0, const Ev& 
     adjoint(P_, evR, 0.0, yR.data(), dc.data(), tmpn.data());
     const double et = eta(mu_);
     double dinf = 0.0;
-    for (int i = 0; i < n; ++i) dinf = std::max(dinf, std::fabs(et * DR2[i] * (xx[i] - xR[i]) + tmpn[i] - zlR[i] + zuR[i]));
+    for (int i = 0; i < n; ++i)
+      if (!fixd[i]) dinf = std::max(dinf, std::fabs(et * DR2[i] * (xx[i] - xR[i]) + tmpn[i] - zlR[i] + zuR[i]));
     for (int r = 0; r < m; ++r) {
       dinf = std::max(dinf, std::fabs(-yR[r] - vlR[r] + vuR[r]));
     }
@@ -1683,7 +1710,8 @@ void Solver::restoration(const Vec& x0, const Vec& s0, const Vec& d0, const Ev& 
       adjoint(P_, evR, 0.0, yR.data(), dc.data(), tmpn.data());
       const double et = eta(mu_);
       double dinf = 0.0;
-      for (int i = 0; i < n; ++i) dinf = std::max(dinf, std::fabs(et * DR2[i] * (xx[i] - xR[i]) + tmpn[i] - zlR[i] + zuR[i]));
+      for (int i = 0; i < n; ++i)
+        if (!fixd[i]) dinf = std::max(dinf, std::fabs(et * DR2[i] * (xx[i] - xR[i]) + tmpn[i] - zlR[i] + zuR[i]));
       for (int r = 0; r < m; ++r) dinf = std::max(dinf, std::fabs(-yR[r] - vlR[r] + vuR[r]));
       for (int r = 0; r < m; ++r) dinf = std::max(dinf, std::fabs(rho - yR[r] - zp[r]));
       for (int r = 0; r < m; ++r) dinf = std::max(dinf, std::fabs(rho + yR[r] - zn[r]));

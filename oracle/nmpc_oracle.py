@@ -618,7 +618,21 @@ class IpoptDense:
         w0 = np.asarray(x0, float).ravel()
         if np.any((np.abs(lbg) < INF) & (lbg == ubg)):
             raise ValueError("equality rows (lbg == ubg) are not supported")
-        xlm, xum = lbx > -INF, ubx < INF
+        # fixed variables (lbx == ubx): IPOPT's default fixed_variable_treatment =
+        # make_parameter (TNLPAdapter) removes them from the NLP -- held at the bound,
+        # no bound multipliers, no step, excluded from the scaling maxima and the
+        # error norms; their lam_x is 0 (IPOPT 3.12, the version CasADi 3.5.5 bundles)
+        fixed = (np.abs(lbx) < INF) & (lbx == ubx)
+        fr = ~fixed
+        nf = int(fr.sum())
+        # free-variable selection; a plain slice when nothing is fixed, so that case
+        # runs the exact same array operations as without the feature
+        F = slice(None) if nf == n else np.flatnonzero(fr)
+
+        def sq(M_):
+            return M_ if nf == n else M_[np.ix_(F, F)]
+        w0 = np.where(fixed, lbx, w0)
+        xlm, xum = (lbx > -INF) & fr, (ubx < INF) & fr
         slm, sum_ = lbg > -INF, ubg < INF
         xl, xu = self._relax(lbx, -1.0), self._relax(ubx, +1.0)
         gl_, gu_ = self._relax(lbg, -1.0), self._relax(ubg, +1.0)
@@ -629,15 +643,15 @@ class IpoptDense:
 
         # gradient-based scaling at the user's starting point
         ev0 = self._evaluate(w0)
-        if not (np.all(np.isfinite(ev0.gradF)) and np.all(np.isfinite(ev0.J))):
+        if not (np.all(np.isfinite(ev0.gradF[F])) and np.all(np.isfinite(ev0.J[:, F]))):
             return self._result(w0, w0, 0, INVALID_NUMBER_DETECTED, 1.0, np.ones(m),
                                 np.zeros(n), np.zeros(n), np.zeros(m), lbx, ubx, [])
-        gmax = np.max(np.abs(ev0.gradF)) if n else 0.0
+        gmax = np.max(np.abs(ev0.gradF[F])) if nf else 0.0
         df = 1.0
         if gmax > o["nlp_scaling_max_gradient"]:
             df = o["nlp_scaling_max_gradient"] / gmax
         df = max(df, o["nlp_scaling_min_value"])
-        rowmax = np.max(np.abs(ev0.J), axis=1) if m else np.zeros(0)
+        rowmax = np.max(np.abs(ev0.J[:, F]), axis=1) if (m and nf) else np.zeros(m)
         dc = np.ones(m)
         if m and np.max(rowmax) > o["nlp_scaling_max_gradient"]:
             with np.errstate(divide="ignore"):
@@ -657,10 +671,10 @@ class IpoptDense:
         vu = np.where(sum_, o["bound_mult_init_val"], 0.0)
         y = np.zeros(m)
         if o["constr_mult_init_max"] > 0 and m > 0:
-            J = dc[:, None] * ev.J
-            bx = df * ev.gradF - zl + zu
+            J = dc[:, None] * ev.J[:, F]
+            bx = (df * ev.gradF - zl + zu)[F]
             bs = vu - vl
-            wx = np.linalg.solve(np.eye(n) + J.T @ J, bx + J.T @ bs)
+            wx = np.linalg.solve(np.eye(nf) + J.T @ J, bx + J.T @ bs)
             y = bs - J @ wx
             if np.max(np.abs(y)) > o["constr_mult_init_max"]:
                 y = np.zeros(m)
@@ -687,7 +701,7 @@ class IpoptDense:
             return val
 
         def grad_lag(gf, J, y_, zl_, zu_, vl_, vu_):
-            return gf + J.T @ y_ - zl_ + zu_, -y_ - vl_ + vu_
+            return np.where(fr, gf + J.T @ y_ - zl_ + zu_, 0.0), -y_ - vl_ + vu_
 
         def compl(x_, s_, zl_, zu_, vl_, vu_, mu_):
             Sxl, Sxu, Ssl, Ssu = slacks(x_, s_)
@@ -765,7 +779,7 @@ class IpoptDense:
 
         def pd_error(x_, s_, d_, gf_, J_, y_, zl_, zu_, vl_, vu_, mu_):
             glx, gls = grad_lag(gf_, J_, y_, zl_, zu_, vl_, vu_)
-            dual = (np.sum(np.abs(glx)) + np.sum(np.abs(gls))) / (n + m)
+            dual = (np.sum(np.abs(glx)) + np.sum(np.abs(gls))) / (nf + m)
             prim = np.sum(np.abs(d_ - s_)) / m if m else 0.0
             nc = nzx + nzs
             cm = np.sum(np.abs(compl(x_, s_, zl_, zu_, vl_, vu_, mu_))) / nc if nc else 0.0
@@ -808,10 +822,10 @@ class IpoptDense:
             # least-squares multipliers of the restoration NLP (constr_mult_init_max)
             yR = np.zeros(m)
             if o["constr_mult_init_max"] > 0 and m > 0:
-                Jfull = np.hstack([JR, -np.eye(m), np.eye(m)])
-                bx = np.concatenate([eta(muR) * DR2 * (xR_ - xR) - zlR + zuR, rho - zp, rho - zn])
+                Jfull = np.hstack([JR[:, F], -np.eye(m), np.eye(m)])
+                bx = np.concatenate([(eta(muR) * DR2 * (xR_ - xR) - zlR + zuR)[F], rho - zp, rho - zn])
                 bs = vuR - vlR
-                wx = np.linalg.solve(np.eye(n + 2 * m) + Jfull.T @ Jfull, bx + Jfull.T @ bs)
+                wx = np.linalg.solve(np.eye(nf + 2 * m) + Jfull.T @ Jfull, bx + Jfull.T @ bs)
                 yR = bs - Jfull @ wx
                 if np.max(np.abs(yR)) > o["constr_mult_init_max"]:
                     yR = np.zeros(m)
@@ -838,7 +852,7 @@ class IpoptDense:
 
             def errR(x_, s_, d_, J_, p_, n_, y_, zl_, zu_, vl_, vu_, zp_, zn_, mu_, mu_c):
                 """(overall error, dual inf, constraint violation, complementarity) of the resto NLP."""
-                glx = eta(mu_) * DR2 * (x_ - xR) + J_.T @ y_ - zl_ + zu_
+                glx = np.where(fr, eta(mu_) * DR2 * (x_ - xR) + J_.T @ y_ - zl_ + zu_, 0.0)
                 gls = -y_ - vl_ + vu_
                 glp, gln = rho - y_ - zp_, rho + y_ - zn_
                 dinf_ = max(amax(glx), amax(gls), amax(glp), amax(gln))
@@ -918,7 +932,7 @@ class IpoptDense:
                 def sub_err(mu_):
                     e_, _, _, _, sd_, sc_, pinf_ = errR(xx, ss, dR, JR, pp, nn, yR, zlR, zuR, vlR, vuR, zp, zn,
                                                         mu_, mu_)
-                    glx = eta(mu_) * DR2 * (xx - xR) + JR.T @ yR - zlR + zuR
+                    glx = np.where(fr, eta(mu_) * DR2 * (xx - xR) + JR.T @ yR - zlR + zuR, 0.0)
                     gls = -yR - vlR + vuR
                     dinf_ = max(amax(glx), amax(gls), amax(rho - yR - zp), amax(rho + yR - zn))
                     cm_ = amax(np.concatenate([compl(xx, ss, zlR, zuR, vlR, vuR, mu_), pp * zp - mu_,
@@ -965,7 +979,7 @@ class IpoptDense:
                     # without 1/D so rows with no bound (D = 0) stay finite
                     M = Wr + np.diag(SigX + delta_) + JR.T @ (Dt[:, None] * JR)
                     try:
-                        fact = np.linalg.cholesky(M)
+                        fact = np.linalg.cholesky(sq(M))
                         break
                     except np.linalg.LinAlgError:
                         if delta_ == 0.0:
@@ -991,7 +1005,8 @@ class IpoptDense:
                     # dy = D~ (J dx + c + rs/D + rp/Sp - rn/Sn), with D~ rs/D = rs * den
                     Dr = Dt * (c_ + rp / Spd - rn / Snd) + rs_ * den
                     rhs = -(gphi + JR.T @ (yR + Dr))
-                    dx_ = np.linalg.solve(fact.T, np.linalg.solve(fact, rhs))
+                    dx_ = np.zeros(n)
+                    dx_[F] = np.linalg.solve(fact.T, np.linalg.solve(fact, rhs[F]))
                     jd = JR @ dx_
                     dy_ = Dt * jd + Dr
                     dp_ = (dy_ - rp) / Spd
@@ -1170,10 +1185,10 @@ class IpoptDense:
             # constr_mult_reset_threshold (default 0: always zero)
             y1 = np.zeros(m)
             if o["constr_mult_reset_threshold"] > 0 and m > 0:
-                J1 = dc[:, None] * evR.J
-                bx = df * evR.gradF - zl1 + zu1
+                J1 = dc[:, None] * evR.J[:, F]
+                bx = (df * evR.gradF - zl1 + zu1)[F]
                 bs = vu1 - vl1
-                wx = np.linalg.solve(np.eye(n) + J1.T @ J1, bx + J1.T @ bs)
+                wx = np.linalg.solve(np.eye(nf) + J1.T @ J1, bx + J1.T @ bs)
                 y1 = bs - J1 @ wx
                 if np.max(np.abs(y1)) > o["constr_mult_reset_threshold"]:
                     y1 = np.zeros(m)
@@ -1254,7 +1269,7 @@ class IpoptDense:
                 D = SigS + delta
                 M = W + np.diag(SigX + delta) + J.T @ (D[:, None] * J)
                 try:
-                    fact = np.linalg.cholesky(M)
+                    fact = np.linalg.cholesky(sq(M))
                     break
                 except np.linalg.LinAlgError:
                     if delta == 0.0:
@@ -1276,8 +1291,9 @@ class IpoptDense:
 
             def solve_dir(rd_):
                 rhs = -(gphi + J.T @ (y + D * rd_ + rs))
-                t = np.linalg.solve(fact, rhs)
-                dx_ = np.linalg.solve(fact.T, t)
+                t = np.linalg.solve(fact, rhs[F])
+                dx_ = np.zeros(n)
+                dx_[F] = np.linalg.solve(fact.T, t)
                 ds_ = J @ dx_ + rd_
                 dy_ = D * ds_ + rs
                 dzl_ = np.where(xlm, mu / Sxl - zl - zl / Sxl * dx_, 0.0)

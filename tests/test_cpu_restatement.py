@@ -145,3 +145,34 @@ def test_equality_rows_rejected_like_the_oracle(cpu):
     assert r["status"][0] == -11
     with pytest.raises(ValueError):
         orc.IpoptDense(prob, orc.REFERENCE_OPTS).solve(np.zeros(prob.nw), lbx, ubx, lbg, ubg, p)
+
+
+@pytest.mark.parametrize("model", ["uav8g", "uav5"])
+def test_fixed_variables_against_oracle(cpu, model):
+    """lbx == ubx (IPOPT make_parameter) in the C++ restatement (fixed controls decoupled
+    in the Riccati recursion) against the numpy oracle (fixed columns removed from the
+    dense system): same statuses and iterations, x within 1e-6, fixed variables exactly
+    at their bound with lam_x 0."""
+    from oracle import nmpc_oracle as orc
+    from nmpc_amd import make_spec, draw_scenarios
+    N = 8
+    prob = orc.make_problem("race_track_2", N=N, T=0.2, model=model)
+    spec = make_spec("race_track_2", N=N, T=0.2, model=model)
+    lbx, ubx, lbg, ubg = orc.bounds(prob)
+    P = draw_scenarios(spec, 4, seed=77)
+    rng = np.random.default_rng(5)
+    lo, hi = lbx.copy(), ubx.copy()
+    idx = rng.choice(len(lbx), 6, replace=False)
+    lo[idx] = hi[idx] = lbx[idx] + rng.uniform(0.2, 0.8, 6) * (ubx[idx] - lbx[idx])
+    lo[0] = hi[0] = 20.0
+    fx = lo == hi
+    W0 = np.zeros((len(P), prob.nw))
+    r = cpu.solve_batch(prob, W0, P, lo, hi, lbg, ubg, orc.REFERENCE_OPTS, threads=2)
+    ref = orc.IpoptDense(prob, orc.REFERENCE_OPTS)
+    for b in range(len(P)):
+        o = ref.solve(W0[b], lo, hi, lbg, ubg, P[b])
+        assert np.all(o["x"][fx] == lo[fx]) and np.all(o["lam_x"][fx] == 0.0)
+        assert np.all(r["x"][b][fx] == lo[fx]) and np.all(r["lam_x"][b][fx] == 0.0)
+        assert r["status"][b] == o["status"] and abs(int(r["iter"][b]) - o["iter"]) <= 1
+        if o["status"] in (0, 1):
+            assert np.max(np.abs(r["x"][b] - o["x"]) / (1 + np.abs(o["x"]))) <= TOL

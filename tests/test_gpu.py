@@ -772,3 +772,59 @@ def test_lam_p_matches_oracle_finite_differences(layout, N, dyn, model, weights)
         assert np.all(np.abs(got - ref) <= 1e-5 * scale), (b, got, ref)
         checked += 1
     assert checked >= 2
+
+
+def _fixed_cases(lbx, ubx, N, nu, seed=5):
+    """bound sets with fixed decision variables (lbx == ubx): the gimbal rates held at 0
+    on every stage, the speed held at 20 on the first three stages, 8 random variables
+    held at random interior values"""
+    rng = np.random.default_rng(seed)
+    cases = []
+    if nu == 6:
+        l1, u1 = lbx.copy(), ubx.copy()
+        for k in range(N):
+            for c in (3, 4, 5):
+                l1[nu * k + c] = u1[nu * k + c] = 0.0
+        cases.append(("gimbal rates fixed", l1, u1))
+    l2, u2 = lbx.copy(), ubx.copy()
+    for k in range(3):
+        l2[nu * k] = u2[nu * k] = 20.0
+    cases.append(("speed fixed", l2, u2))
+    l3, u3 = lbx.copy(), ubx.copy()
+    idx = rng.choice(len(lbx), 8, replace=False)
+    l3[idx] = u3[idx] = lbx[idx] + rng.uniform(0.2, 0.8, 8) * (ubx[idx] - lbx[idx])
+    cases.append(("random fixed", l3, u3))
+    return cases
+
+
+@pytest.mark.parametrize("model", ["uav8g", "uav5"])
+def test_fixed_variables_make_parameter_match_oracle(model):
+    """lbx == ubx (IPOPT's default fixed_variable_treatment = make_parameter: the variable
+    leaves the NLP -- held at the bound, no step, no bound multipliers, out of the scaling
+    and the error norms -- and its lam_x is 0, IPOPT 3.12 as bundled by CasADi 3.5.5),
+    against the oracle's dense restatement of the same treatment."""
+    from nmpc_amd import make_spec, draw_scenarios
+
+    N = 10
+    spec = make_spec("race_track_2", N=N, T=0.2, model=model)
+    prob = orc.make_problem("race_track_2", N=N, T=0.2, model=model)
+    B = 6
+    P = draw_scenarios(spec, B, seed=77)
+    lbx, ubx, lbg, ubg = spec.bounds()
+    ref = orc.IpoptDense(prob, orc.REFERENCE_OPTS)
+    s = _solver(spec)
+    for name, lo, hi in _fixed_cases(lbx, ubx, N, spec.nu):
+        sol = s(x0=np.zeros(spec.nw), lbx=lo, ubx=hi, lbg=lbg, ubg=ubg, p=P.T)
+        st, its = s.stats()["status_code"], s.stats()["iter_count"]
+        fx = lo == hi
+        for b in range(B):
+            r = ref.solve(np.zeros(spec.nw), lo, hi, lbg, ubg, P[b])
+            assert int(st[b]) == r["status"], (name, b, st[b], r["status"])
+            assert abs(int(its[b]) - r["iter"]) <= 1, (name, b, its[b], r["iter"])
+            assert np.all(sol["x"][fx, b] == lo[fx]) and np.all(sol["lam_x"][fx, b] == 0.0)
+            if r["status"] in (0, 1):
+                assert _rel(sol["x"][:, b], r["x"]) <= TOL, name
+                assert abs(sol["f"][0, b] - r["f"]) <= TOL * (1 + abs(r["f"]))
+                assert _rel(sol["lam_x"][:, b], r["lam_x"]) <= 1e-5, name
+        print(f"{model} {name}: statuses {dict(zip(*np.unique(st, return_counts=True)))}, "
+              f"iterations {its.tolist()}")

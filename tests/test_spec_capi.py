@@ -102,6 +102,9 @@ def test_default_options_are_ipopt_defaults():
         make_options({"ipopt": {"no_such_option": 1}})
     with pytest.raises(ValueError):
         make_options({"ipopt": {"hessian_approximation": "limited-memory"}})
+    make_options({"ipopt": {"fixed_variable_treatment": "make_parameter"}})  # IPOPT default: accepted
+    with pytest.raises(ValueError):
+        make_options({"ipopt": {"fixed_variable_treatment": "relax_bounds"}})
 
 
 def _desc(**kw):
