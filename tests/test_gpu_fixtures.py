@@ -191,3 +191,48 @@ def test_config3_closed_loop_at_bench_scale_matches_cpu_restatement():
     assert agree >= 0.99
     assert full >= 0.9 * B
     assert matched >= 0.95 * B * K
+
+
+def test_config3_fov_error_sums_match_oracle():
+    """The reference's only printed result: the run's sum of |FOV centre - target|
+    (Python/NMPC_TT.py:397-400,433-440), here per scenario over the fixture's 20
+    closed-loop steps -- the device loop's FOV history (nmpc_closed_loop_dev) against
+    the same sum recomputed from the oracle's own trajectory (tests/golden
+    closed_loop_config3), for every chain that converges at all 20 steps on both sides."""
+    import sys
+    import torch
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    from oracle import nmpc_oracle as orc
+
+    z = _load("config3")
+    spec, s = _solver(3)
+    B, K = z["status"].shape
+    f64 = dict(dtype=torch.float64, device="cuda")
+    bnd = [torch.tensor(v, **f64) for v in spec.bounds()]
+    hist = {"fov": torch.empty(K, B, **f64), "status": torch.empty(K, B, dtype=torch.int32, device="cuda")}
+    s.closed_loop_device(K, *bnd, torch.tensor(z["P"], **f64), torch.zeros(B, spec.nw, **f64),
+                         torch.full((B,), float(z["vt"]), **f64), torch.full((B,), float(z["wt"]), **f64), hist)
+    torch.cuda.synchronize()
+    fov, st = hist["fov"].cpu().numpy(), hist["status"].cpu().numpy()
+    prob = orc.make_problem("race_track_2", N=spec.N, T=spec.T)
+    nx, compared, worst, tot_g, tot_o = 8, 0, 0.0, 0.0, 0.0
+    for b in range(B):
+        if not (np.all(st[:, b] == z["status"][b]) and np.all(np.isin(z["status"][b], (0, 1)))):
+            continue  # a max-iter / infeasible step returns an unconverged u0: not comparable
+        ref = 0.0
+        for k in range(K):
+            p = z["p"][b, k]
+            x1, _, _ = orc.shift_timestep(prob, p[:nx], z["x"][b, k].reshape(spec.N, 6).T, p[nx:nx + 3],
+                                          con_t=(float(z["vt"]), float(z["wt"])))
+            xe, ye = orc.fov_centre(x1)
+            ref += float(np.hypot(xe - p[nx], ye - p[nx + 1]))
+        got = float(fov[:, b].sum())
+        worst = max(worst, abs(got - ref) / (1 + abs(ref)))
+        tot_g, tot_o = tot_g + got, tot_o + ref
+        compared += 1
+    print(f"\nFOV-error sums over {K} steps: {compared}/{B} scenarios compared; total {tot_g:.6f} (GPU) vs "
+          f"{tot_o:.6f} (oracle); max per-scenario rel. difference {worst:.2e}")
+    assert compared >= 0.75 * B
+    assert worst <= 1e-6
