@@ -262,7 +262,7 @@ def main():
         if not cold:
             solver.shift_device(p, out["x"], w, v_t, w_t, stream=stream)
         if world > 1:  # per-step gather of (u0, f, status)
-            gather_rows(pack_result(out["x"], out["f"], out["status"], spec.nu), world)
+            gather_rows(pack_result(out["x"], out["f"], out["status"], spec.nu), world, total=B * world)
         hist["u"][k].zero_(); hist["u"][k][:, :spec.nu].copy_(out["x"][:, :spec.nu]); hist["f"][k].copy_(out["f"])
         hist["iters"][k].copy_(out["iters"]); hist["status"][k].copy_(out["status"])
 
@@ -273,7 +273,7 @@ def main():
         if timed_events is not None:
             timed_events[1].record(stream)
         if world > 1:  # the only exchange: final gather of every step's (u0, f, status)
-            gather_closed_loop(hist, world)
+            gather_closed_loop(hist, world, total=B * world)
 
     def barrier_sync():
         torch.cuda.synchronize()

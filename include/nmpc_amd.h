@@ -208,7 +208,8 @@ int nmpc_shift_dev(nmpc_handle* h, int32_t B, double* p, int64_t ld_p,
  *          do not depend on it.  Putting the longest expected chains first (e.g.
  *          sorted by the previous launch's iterations, nmpc_amd.schedule) keeps a
  *          long chain from starting after the first wave of slots has drained.
- *          Entries outside [0,B) are skipped; duplicates are the caller's error. */
+ *          Entries outside [0,B) are skipped; a duplicated or missing scenario leaves
+ *          some scenario short of its K steps, which nmpc_closed_loop_info reports. */
 int nmpc_closed_loop_dev(nmpc_handle* h, int32_t B, int32_t K,
                          const double* lbx, int64_t ld_lbx, const double* ubx, int64_t ld_ubx,
                          const double* lbg, int64_t ld_lbg, const double* ubg, int64_t ld_ubg,
@@ -218,8 +219,9 @@ int nmpc_closed_loop_dev(nmpc_handle* h, int32_t B, int32_t K,
                          double* u_hist, double* x_hist, double* f_hist, double* fov_hist,
                          int32_t* status_hist, int32_t* iters_hist, const int32_t* order, void* stream);
 
-/* Scheduling of the last nmpc_closed_loop_dev launch (synchronises the device when
- * sched_err or steps_done is requested; any pointer may be NULL).
+/* Scheduling of the last nmpc_closed_loop_dev launch (any pointer may be NULL).  When
+ * sched_err or steps_done is requested it first synchronises the stream that launch
+ * was enqueued on (hipStreamSynchronize), so it is valid for non-blocking streams.
  *   policy: 0 = one workgroup per scenario running its K steps back to back (B <=
  *     resident waves, a device without exactly 8 XCDs, or NMPC_CLOSED_LOOP=static);
  *     1 = step queues: persistent waves claim (scenario, step) pairs whose previous step
@@ -227,9 +229,10 @@ int nmpc_closed_loop_dev(nmpc_handle* h, int32_t B, int32_t K,
  *   resident: waves the closed-loop kernel keeps resident (occupancy x CUs; 0 before
  *     the first launch).  waves: workgroups the last launch started.
  *   sched_err: bit 0 a wave gave up waiting for a published step, bit 1 a scenario did
- *     not complete its K steps (its unrun steps carry status NMPC_STATUS_NOT_RUN and NaN
- *     f / u in the histories).  0 on success.
- *   steps_done: closed-loop steps completed (must equal B*K). */
+ *     not complete its K steps (its unrun steps carry status and iterations
+ *     NMPC_STATUS_NOT_RUN and NaN f / fov / u / x in the histories).  0 on success.
+ *   steps_done: closed-loop steps completed, counted per scenario by a check kernel
+ *     after either policy's launch (must equal B*K; 64-bit). */
 #define NMPC_STATUS_NOT_RUN (-1000)
 int nmpc_closed_loop_info(nmpc_handle* h, int32_t* policy, int32_t* resident, int32_t* sched_err,
                           int32_t* waves, int64_t* steps_done);

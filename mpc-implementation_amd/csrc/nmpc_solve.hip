@@ -14,7 +14,9 @@
 //   * matrix entries (lane = 8*i + j) in the Riccati backward sweep;
 //   * rows / controls (strided) for fraction-to-boundary, barrier terms,
 //     multiplier updates and optimality-error reductions.
-// Per-scenario iterate, sensitivities and the Riccati factors live in LDS.
+// The hot row vectors, trajectories and the current Riccati stage operands live in
+// LDS; control vectors, the per-stage Riccati factors (K, R~, Q) and the restoration /
+// watchdog copies live in a per-scenario global workspace.
 //
 // Algorithm: the IPOPT restatement of oracle/nmpc_oracle.py::IpoptDense,
 // step for step (same options, same decisions), except that the Newton
@@ -3185,6 +3187,7 @@ struct Loop {
   long long ld_ps;
   int *st_hist, *it_hist;            // K x B (nullable)
   const int* order;                  // dispatch order: workgroup g runs scenario order[g] (nullable)
+  int* done;                         // B: steps completed per scenario (completion guard; nullable)
   unsigned long long* times;         // diagnostics (NMPC_STEP_TIMES): K x B x {start, end, XCC_ID|wave<<8}
 };
 
@@ -3282,6 +3285,9 @@ __global__ __launch_bounds__(WAVE, CAP::wpe) void nmpc_closed_loop_kernel(const 
       unsigned long long* t = lp.times + ((long long)k * B + b) * 3;
       t[0] = t0; t[1] = __builtin_amdgcn_s_memrealtime(); t[2] = blockIdx.x;
     }
+    // completion guard (nmpc_sched_check_kernel): a duplicated or missing dispatch
+    // entry leaves some scenario short of its K steps, which the check reports
+    if (lp.done && threadIdx.x == 0) lp.done[b] = k + 1;
   }
 }
 
@@ -3317,8 +3323,8 @@ struct SchedQ {
   int* tail;  // 2 x NXCD x K: published count
   int* resv;  // 2 x NXCD x K: reserved count
   int* ring;  // 2 x NXCD x K x BX scenario ids (-1 = not yet written)
-  int* err;   // [0]: 1 a wave gave up waiting, 2 a scenario did not complete its K steps;
-              // [1]: closed-loop steps completed (nmpc_sched_check_kernel)
+  int* err;   // [0]: 1 a wave gave up waiting, 2 a scenario did not complete its K steps
+  unsigned long long* ndone;  // closed-loop steps completed (nmpc_sched_check_kernel; 64-bit: B*K may exceed 2^31)
   int* done;  // B: steps completed per scenario
   int BX;     // ring capacity per queue = ceil(B / NXCD)
   int one_set;  // test hook (NMPC_SCHED_TEST_ONE_SET): only the waves on XCD 0 run, so
@@ -3455,27 +3461,40 @@ __global__ void nmpc_sched_init_kernel(int B, int K, const int* order, SchedQ q)
     q.tail[i] = j == 0 ? nset : 0;
     q.resv[i] = j == 0 ? nset : 0;
   }
-  if (i == 0) { q.err[0] = 0; q.err[1] = 0; }
+  if (i == 0) { q.err[0] = 0; *q.ndone = 0; }
   if (i < B) q.done[i] = 0;
 }
 
-// After a step-queue launch (same stream): every scenario must have completed its K
-// steps (Python/NMPC_TT.py:348-402 advances every scenario K times).  A scenario that
-// did not sets err[0] |= 2, and its unrun steps are marked in the histories
-// (status NMPC_STATUS_NOT_RUN, f and u NaN) so nothing is left uninitialised.
-__global__ void nmpc_sched_check_kernel(int B, int K, SchedQ q, int* st_hist, double* f_hist, double* u_hist) {
+// completion-guard state of a one-workgroup-per-scenario launch (no queues)
+__global__ void nmpc_guard_init_kernel(int B, SchedQ q) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i == 0) { q.err[0] = 0; *q.ndone = 0; }
+  if (i < B) q.done[i] = 0;
+}
+
+// After a closed-loop launch (same stream, either policy): every scenario must have
+// completed its K steps (Python/NMPC_TT.py:348-402 advances every scenario K times).
+// A scenario that did not sets err[0] |= 2, and its unrun steps are marked in every
+// history (status / iterations NMPC_STATUS_NOT_RUN; f, fov, u, x NaN) so nothing is
+// left uninitialised.
+__global__ void nmpc_sched_check_kernel(int B, int K, SchedQ q, const Loop lp) {
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= B) return;
   const int d = q.done[b];
-  atomicAdd(q.err + 1, d);
+  atomicAdd(q.ndone, (unsigned long long)(d < 0 ? 0 : d));
   if (d == K) return;
   atomicOr(q.err, 2);
+  const double nan = __builtin_nan("");
   for (int k = d < 0 ? 0 : d; k < K; ++k) {
     const long long kb = (long long)k * B + b;
-    if (st_hist) st_hist[kb] = NMPC_STATUS_NOT_RUN;
-    if (f_hist) f_hist[kb] = __builtin_nan("");
-    if (u_hist)
-      for (int c = 0; c < 6; ++c) u_hist[kb * 6 + c] = __builtin_nan("");
+    if (lp.st_hist) lp.st_hist[kb] = NMPC_STATUS_NOT_RUN;
+    if (lp.it_hist) lp.it_hist[kb] = NMPC_STATUS_NOT_RUN;
+    if (lp.f_hist) lp.f_hist[kb] = nan;
+    if (lp.fov_hist) lp.fov_hist[kb] = nan;
+    if (lp.u_hist)
+      for (int c = 0; c < 6; ++c) lp.u_hist[kb * 6 + c] = nan;
+    if (lp.x_hist)
+      for (int c = 0; c < 8; ++c) lp.x_hist[kb * 8 + c] = nan;
   }
 }
 
@@ -3576,7 +3595,9 @@ struct nmpc_handle {
   int last_policy = 0;         // last closed-loop launch: 0 one workgroup per scenario, 1 step queues
   int last_waves = 0;          // workgroups launched by the last closed-loop launch
   long long last_steps = 0;    // B*K of the last closed-loop launch
-  int* last_err = nullptr;     // device flags of the last step-queue launch (SchedQ::err)
+  int* last_err = nullptr;     // device flags of the last closed-loop launch (SchedQ::err)
+  unsigned long long* last_ndone = nullptr;  // its completed-step counter (SchedQ::ndone)
+  hipStream_t last_stream = nullptr;         // the stream it was enqueued on
   unsigned long long* dtimes = nullptr;  // diagnostics: step timestamps of the last closed loop
   size_t times_bytes = 0, times_n = 0;
   int ws_doubles = 0;
@@ -3736,13 +3757,21 @@ int nmpc_closed_loop_info(nmpc_handle* h, int32_t* policy, int32_t* resident, in
   if (policy) *policy = h->last_policy;
   if (resident) *resident = h->resident;
   if (waves) *waves = h->last_waves;
-  if (sched_err || steps_done) {
-    int e[2] = {0, 0};
-    if (h->last_err && hipMemcpy(e, h->last_err, 2 * sizeof(int), hipMemcpyDeviceToHost) != hipSuccess)
+  if ((sched_err || steps_done) && h->last_err) {
+    // the flags are written by kernels on the launch's stream: wait for that stream
+    // (a non-blocking stream does not synchronise with the null stream's memcpy)
+    if (hipStreamSynchronize(h->last_stream) != hipSuccess)
+      return fail(NMPC_E_HIP, "synchronising the closed-loop stream");
+    int e = 0;
+    unsigned long long nd = 0;
+    if (hipMemcpy(&e, h->last_err, sizeof(int), hipMemcpyDeviceToHost) != hipSuccess ||
+        hipMemcpy(&nd, h->last_ndone, sizeof(nd), hipMemcpyDeviceToHost) != hipSuccess)
       return fail(NMPC_E_HIP, "reading the scheduler flags");
-    if (sched_err) *sched_err = e[0];
-    // one workgroup per scenario runs all K steps of its scenario by construction
-    if (steps_done) *steps_done = h->last_err ? (int64_t)e[1] : (int64_t)h->last_steps;
+    if (sched_err) *sched_err = e;
+    if (steps_done) *steps_done = (int64_t)nd;
+  } else {
+    if (sched_err) *sched_err = 0;
+    if (steps_done) *steps_done = 0;
   }
   return NMPC_OK;
 }
@@ -3949,6 +3978,7 @@ int nmpc_closed_loop_dev(nmpc_handle* h, int32_t B, int32_t K, const double* lbx
   lp.pstep = p_step; lp.ld_ps = ld_ps;
   lp.st_hist = status_hist; lp.it_hist = iters_hist;
   lp.order = order;
+  lp.done = nullptr;
   lp.times = nullptr;
   if (std::getenv("NMPC_STEP_TIMES")) {  // diagnostics: per-(step, scenario) realtime stamps (100 MHz)
     const size_t need = (size_t)K * B * 3 * sizeof(unsigned long long);
@@ -3985,25 +4015,33 @@ int nmpc_closed_loop_dev(nmpc_handle* h, int32_t B, int32_t K, const double* lbx
   const bool use_q = (B > h->resident) && h->resident >= NXCD && h->nxcc == NXCD &&
                      !(pol && std::strcmp(pol, "static") == 0);
   h->last_steps = (long long)B * K;
+  // scheduler / completion-guard state: [ndone (u64)][err, pad][done (B)][queues]
+  const int BX = use_q ? (B + NXCD - 1) / NXCD : 0;
+  const size_t nint = 4 + (size_t)B + (use_q ? (size_t)6 * NXCD * K + (size_t)2 * NXCD * K * BX : 0);
+  if (nint * sizeof(int) > h->sched_bytes) {
+    if (h->dsched) hipFree(h->dsched);
+    h->dsched = nullptr; h->sched_bytes = 0;
+    if (hipMalloc(&h->dsched, nint * sizeof(int)) != hipSuccess) return fail(NMPC_E_NOMEM, "hipMalloc scheduler");
+    h->sched_bytes = nint * sizeof(int);
+  }
+  SchedQ q;
+  std::memset(&q, 0, sizeof(q));
+  q.ndone = (unsigned long long*)h->dsched;
+  q.err = h->dsched + 2;
+  q.done = h->dsched + 4;
+  const int thr = 256;
+  h->last_err = q.err;
+  h->last_ndone = q.ndone;
+  h->last_stream = (hipStream_t)stream;
   if (use_q) {
-    const int BX = (B + NXCD - 1) / NXCD;
-    const size_t nint = (size_t)6 * NXCD * K + (size_t)2 * NXCD * K * BX + 2 + (size_t)B;
-    if (nint * sizeof(int) > h->sched_bytes) {
-      if (h->dsched) hipFree(h->dsched);
-      h->dsched = nullptr; h->sched_bytes = 0;
-      if (hipMalloc(&h->dsched, nint * sizeof(int)) != hipSuccess) return fail(NMPC_E_NOMEM, "hipMalloc scheduler");
-      h->sched_bytes = nint * sizeof(int);
-    }
-    SchedQ q;
-    q.head = h->dsched; q.tail = q.head + 2 * NXCD * K; q.resv = q.tail + 2 * NXCD * K;
-    q.ring = q.resv + 2 * NXCD * K; q.err = q.ring + (size_t)2 * NXCD * K * BX; q.done = q.err + 2; q.BX = BX;
+    q.head = q.done + B; q.tail = q.head + 2 * NXCD * K; q.resv = q.tail + 2 * NXCD * K;
+    q.ring = q.resv + 2 * NXCD * K; q.BX = BX;
     // hot family threshold: half of max_iter (NMPC_SCHED_HOT overrides; 0 = one family only)
     q.hot_iters = h->hp.o.max_iter / 2 > 0 ? h->hp.o.max_iter / 2 : 1;
     if (const char* hv = std::getenv("NMPC_SCHED_HOT")) q.hot_iters = std::atoi(hv);
     const char* one = std::getenv("NMPC_SCHED_TEST_ONE_SET");
     q.one_set = (one && std::atoi(one) != 0) ? 1 : 0;
     const long long n = (long long)NXCD * K * BX;
-    const int thr = 256;
     hipLaunchKernelGGL(nmpc_sched_init_kernel, dim3((unsigned)((n + thr - 1) / thr)), dim3(thr), 0,
                        (hipStream_t)stream, (int)B, (int)K, (const int*)order, q);
     // persistent waves: all resident ones.  NMPC_SCHED_WAVES (a diagnostic) launches
@@ -4017,18 +4055,21 @@ int nmpc_closed_loop_dev(nmpc_handle* h, int32_t B, int32_t K, const double* lbx
     }
     hipLaunchKernelGGL(h->sched, dim3(waves), dim3(WAVE), h->lds_bytes, (hipStream_t)stream,
                        (const Params*)h->dprm, (int)B, io, lp, q);
-    hipLaunchKernelGGL(nmpc_sched_check_kernel, dim3((B + thr - 1) / thr), dim3(thr), 0, (hipStream_t)stream,
-                       (int)B, (int)K, q, status_hist, f_hist, u_hist);
     h->last_policy = 1;
     h->last_waves = waves;
-    h->last_err = q.err;
   } else {
     h->last_policy = 0;
     h->last_waves = B;
-    h->last_err = nullptr;
+    lp.done = q.done;
+    hipLaunchKernelGGL(nmpc_guard_init_kernel, dim3((B + thr - 1) / thr), dim3(thr), 0, (hipStream_t)stream,
+                       (int)B, q);
     hipLaunchKernelGGL(h->loop, dim3(B), dim3(WAVE), h->lds_bytes, (hipStream_t)stream,
                        (const Params*)h->dprm, (int)B, io, lp);
   }
+  // completion guard, both policies: every scenario ran its K steps, else err |= 2 and
+  // the unrun steps are marked in the histories
+  hipLaunchKernelGGL(nmpc_sched_check_kernel, dim3((B + thr - 1) / thr), dim3(thr), 0, (hipStream_t)stream,
+                     (int)B, (int)K, q, lp);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return fail(NMPC_E_HIP, std::string("closed-loop launch: ") + hipGetErrorString(e));
   return NMPC_OK;

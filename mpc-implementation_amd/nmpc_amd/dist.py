@@ -29,12 +29,31 @@ def pack_result(x, f, status, nu: int = 6):
     return torch.cat([u0, f[:, None], status[:, None].to(x.dtype)], dim=1).contiguous()
 
 
-def gather_rows(local, world: int, group=None):
-    """All-gather equal-sized (B, k) row blocks from every rank -> (world*B, k)."""
+def shard_sizes(total: int, world: int) -> list[int]:
+    """Rows each rank holds under shard(): the first total % world ranks one more."""
+    return [shard(total, world, r).stop - shard(total, world, r).start for r in range(world)]
+
+
+def gather_rows(local, world: int, group=None, total: int | None = None):
+    """All-gather the (B_r, k) row blocks of every rank -> (sum B_r, k), in rank order.
+
+    ``total`` (the global row count) gives the per-rank sizes of shard(); omitted, every
+    block must have the same size.  Unequal blocks (total % world != 0) are padded to the
+    largest one, gathered in one collective (all_gather_into_tensor over RCCL needs equal
+    sizes), and the padding is dropped again."""
     import torch
     import torch.distributed as dist
 
-    out = torch.empty((world * local.shape[0],) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
+    sizes = shard_sizes(total, world) if total is not None else [local.shape[0]] * world
+    rank = dist.get_rank(group)
+    if local.shape[0] != sizes[rank]:
+        raise ValueError(f"rank {rank} holds {local.shape[0]} rows, shard() gives it {sizes[rank]}")
+    bmax = max(sizes)
+    if local.shape[0] < bmax:
+        pad = torch.zeros((bmax - local.shape[0],) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
+        local = torch.cat([local, pad], dim=0)
+    local = local.contiguous()
+    out = torch.empty((world * bmax,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
     if dist.get_backend(group) == "nccl":
         dist.all_gather_into_tensor(out, local, group=group)
     else:  # gloo (CPU tests, single-GPU rehearsal): staged through host memory
@@ -42,7 +61,9 @@ def gather_rows(local, world: int, group=None):
         parts = [torch.empty_like(host) for _ in range(world)]
         dist.all_gather(parts, host, group=group)
         out.copy_(torch.cat(parts, dim=0))
-    return out
+    if all(n == bmax for n in sizes):
+        return out
+    return torch.cat([out[r * bmax:r * bmax + n] for r, n in enumerate(sizes)], dim=0)
 
 
 def pack_closed_loop(hist):
@@ -51,11 +72,12 @@ def pack_closed_loop(hist):
     import torch
 
     u, f, st = hist["u"], hist["f"], hist["status"]
-    B = u.shape[1]
-    return torch.cat([u.permute(1, 0, 2).reshape(B, -1), f.t(), st.t().to(u.dtype)], dim=1).contiguous()
+    K, B = u.shape[0], u.shape[1]  # B may be 0 (a rank with an empty shard)
+    return torch.cat([u.permute(1, 0, 2).reshape(B, K * u.shape[2]), f.t(), st.t().to(u.dtype)], dim=1).contiguous()
 
 
-def gather_closed_loop(hist, world: int, group=None):
+def gather_closed_loop(hist, world: int, group=None, total: int | None = None):
     """The fused mode's only exchange: one all-gather of every rank's packed
-    histories after its K-step launch -> (world*B, 8K) on every rank."""
-    return gather_rows(pack_closed_loop(hist), world, group)
+    histories after its K-step launch -> (total, 8K) on every rank (``total``
+    scenarios over all ranks, sharded by shard(); None = equal shards)."""
+    return gather_rows(pack_closed_loop(hist), world, group, total)

@@ -303,6 +303,10 @@ class Solver:
         if order is not None:
             assert order.dtype == torch.int32 and order.is_cuda and order.is_contiguous()
             assert tuple(order.shape) == (B,), tuple(order.shape)
+            # a dispatch order must be a permutation: a duplicate would run one scenario
+            # on two waves at once (the completion check would still flag the missing one)
+            if not torch.equal(torch.sort(order).values, torch.arange(B, dtype=torch.int32, device=order.device)):
+                raise ValueError("order must be a permutation of range(B)")
         if stream is None:
             stream = torch.cuda.current_stream()
         _lib.check(L.nmpc_closed_loop_dev(self._h, B, K, *ins, C.c_void_p(p.data_ptr()), self.np,
@@ -326,7 +330,7 @@ class Solver:
 
     def closed_loop_info(self):
         """Scheduling of the last closed_loop_device launch (nmpc_closed_loop_info;
-        synchronises the device)."""
+        synchronises the stream that launch was enqueued on before reading its flags)."""
         pol, res, err, wav, done = C.c_int32(), C.c_int32(), C.c_int32(), C.c_int32(), C.c_int64()
         _lib.check(_lib.lib().nmpc_closed_loop_info(self._h, C.byref(pol), C.byref(res), C.byref(err),
                                                     C.byref(wav), C.byref(done)))

@@ -35,6 +35,9 @@ _lib = None
 def lib():
     global _lib
     if _lib is None:
+        if not os.path.exists(LIB_PATH):  # the checker is built on demand (not part of the product build)
+            import subprocess
+            subprocess.run(["make", "-s", "-C", os.path.dirname(LIB_PATH)], check=False)
         if not os.path.exists(LIB_PATH):
             raise RuntimeError(f"{LIB_PATH} missing: run `make -C oracle` or python __graft_entry__.py")
         L = C.CDLL(LIB_PATH)

@@ -1,0 +1,160 @@
+"""Reference-run fixtures: the reference scripts' OWN closed loops, restated literally
+and driven through the oracle (test infrastructure only).
+
+Every parity case elsewhere draws synthetic scenarios; these are the three runs the
+reference itself performs, with the inputs its scripts hard-code:
+
+  nmpc_tt       Python/NMPC_TT.py: x0 = [90,150,80,0,0,0,0,0] (:321), target
+                (100,150,0) (:316-318), T = 1, N = 15 (:57-58), 3 obstacles r = 30
+                (:224-231), target controls con_t = (12, 0.01) (:25), 700 steps (:339)
+  10_obstacles  Python/10_obstacles.py: x0 = [99,150,80,0,...] (:376), T = 0.2 (:95),
+                N = 15, 10 obstacle rows (3 active, r = 100, :247-269), the
+                mpc_iter-keyed turn schedule (:28-60), 1,595 steps (:388)
+  race_track_2  Python/Race Track 2.py: x0 = [99,150,80,0,...] (:356), T = 0.2,
+                N = 15, all 10 obstacles active (r = 50, :223-244), schedule
+                (:28-36), 2,000 steps (:363)
+
+Each step is the reference loop body (NMPC_TT.py:348-402): p = [x0; xs] (:350-353),
+warm start vec(u0) (:355-356), solve (:358-365) with the script's own bound vectors
+(:269-306, the literal N = 15 strides), u = reshape(x, 6, N) (:367), then
+shift_timestep (:13-30) with the script's con_t for the current mpc_iter.  The FOV
+error of step i is |FOV centre of x0 after step i - target before step i|
+(:399-402, :433-435), and the run's printed result is its sum (:438-440).
+
+Recorded per step: p (the solver's parameter input; the warm start is the shift of
+the previous step's x, reconstructed exactly by the test), status, iterations,
+x, f, and the FOV error; plus the run's FOV-error sum.
+
+Solvers (`--solver`):
+  numpy  oracle/nmpc_oracle.py IpoptDense (dense single-shooting IPOPT
+         restatement) -- the committed fixtures (ref_run_<name>.npz);
+  cpp    oracle/cpu_ipopt.cpp (compiled restatement with the Riccati step),
+         written to ref_run_<name>_cpp.npz for cross-checks, not committed.
+
+    python tests/golden/gen_reference_runs.py [nmpc_tt|10_obstacles|race_track_2|all] [--solver numpy]
+"""
+import argparse
+import math
+import multiprocessing as mp
+import os
+import sys
+import time
+import warnings
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "mpc-implementation_amd"))
+
+X0_NMPC_TT = [90.0, 150.0, 80.0, 0.0, 0.0, 0.0, 0.0, 0.0]   # Python/NMPC_TT.py:321
+X0_10_OBS = [99.0, 150.0, 80.0, 0.0, 0.0, 0.0, 0.0, 0.0]    # Python/10_obstacles.py:376, Race Track 2.py:356
+XS0 = [100.0, 150.0, 0.0]                                    # NMPC_TT.py:316-318 (same in both others)
+
+RUNS = {
+    "nmpc_tt": dict(layout="nmpc_tt", N=15, T=1.0, x0=X0_NMPC_TT, K=700),
+    "10_obstacles": dict(layout="10_obstacles", N=15, T=0.2, x0=X0_10_OBS, K=1595),
+    "race_track_2": dict(layout="race_track_2", N=15, T=0.2, x0=X0_10_OBS, K=2000),
+}
+
+
+def literal_bounds(name, N=15):
+    """The scripts' own bound vectors, built with their literal slices
+    (Python/NMPC_TT.py:269-306: lbg[0:128:8] ...; 10_obstacles.py / Race Track 2.py
+    :314-351: lbg[0:240:15] ...)."""
+    pi = math.pi
+    nu = 6
+    lbx, ubx = np.zeros(nu * N), np.zeros(nu * N)
+    for c, (lo, hi) in enumerate([(14, 30), (-pi / 30, pi / 30), (-pi / 21, pi / 21),
+                                  (-pi / 30, pi / 30), (-pi / 30, pi / 30), (-pi / 30, pi / 30)]):
+        lbx[c:nu * N:nu], ubx[c:nu * N:nu] = lo, hi
+    m, stop = (8, 128) if name == "nmpc_tt" else (15, 240)
+    lbg, ubg = np.zeros(m * (N + 1)), np.zeros(m * (N + 1))
+    for r, (lo, hi) in enumerate([(75, 150), (-0.2618, 0.2618), (-pi / 6, pi / 6), (-pi / 6, pi / 6),
+                                  (-pi / 2, pi / 2)]):
+        lbg[r:stop:m], ubg[r:stop:m] = lo, hi
+    for r in range(5, m):  # obstacle rows: (-inf, 0]
+        lbg[r:stop:m], ubg[r:stop:m] = -np.inf, 0.0
+    return lbx, ubx, lbg, ubg
+
+
+def warm_start(x_prev, N=15, nu=6):
+    """u0 <- [u[:,1:], u[:,-1]] (Python/NMPC_TT.py:20-23) of the previous solution, as vec."""
+    U = x_prev.reshape(N, nu)
+    return np.concatenate([U[1:], U[-1:]]).ravel()
+
+
+def run(name, solver="numpy", K=None, log_every=100):
+    warnings.simplefilter("error", RuntimeWarning)  # no silent NaN/inf arithmetic in the checker
+    from threadpoolctl import threadpool_limits
+    from oracle import nmpc_oracle as orc
+    from nmpc_amd.targets import con_t
+
+    threadpool_limits(1)
+    c = RUNS[name]
+    K = K or c["K"]
+    prob = orc.make_problem(c["layout"], N=c["N"], T=c["T"])
+    lbx, ubx, lbg, ubg = literal_bounds(name, c["N"])
+    if solver == "numpy":
+        ipo = orc.IpoptDense(prob, orc.REFERENCE_OPTS)
+
+        def solve(w, p):
+            r = ipo.solve(w, lbx, ubx, lbg, ubg, p)
+            return r["status"], r["iter"], r["x"], r["f"]
+    else:
+        from oracle import cpu_ipopt
+
+        def solve(w, p):
+            r = cpu_ipopt.solve_batch(prob, w[None], p[None], lbx, ubx, lbg, ubg, orc.REFERENCE_OPTS, threads=1)
+            return int(r["status"][0]), int(r["iter"][0]), r["x"][0], float(r["f"][0])
+    nx, N, nu = 8, c["N"], 6
+    x0, xs = np.array(c["x0"]), np.array(XS0)
+    w = np.zeros(nu * N)   # u0 = zeros (Python/NMPC_TT.py:329)
+    rec = {k: [] for k in ("p", "status", "iter", "x", "f", "fov")}
+    t0 = time.time()
+    for it in range(K):
+        p = np.concatenate([x0, xs])
+        st, ni, x, f = solve(w, p)
+        U = x.reshape(N, nu).T   # ca.reshape(sol['x'], 6, N)
+        x1, _, xs1 = orc.shift_timestep(prob, x0, U, xs, con_t=con_t(name, it))
+        xe, ye = orc.fov_centre(x1)
+        rec["p"].append(p); rec["status"].append(st); rec["iter"].append(ni)
+        rec["x"].append(x.copy()); rec["f"].append(f)
+        rec["fov"].append(math.sqrt((xe - xs[0]) ** 2 + (ye - xs[1]) ** 2))
+        x0, xs, w = x1, xs1, warm_start(x, N, nu)
+        if log_every and (it + 1) % log_every == 0:
+            print(f"  {name}: {it + 1}/{K} steps, {time.time() - t0:.0f}s", flush=True)
+    out = {k: np.array(v) for k, v in rec.items()}
+    out.update(name=name, solver=solver, K=K, N=N, T=c["T"], fov_sum=float(np.sum(out["fov"])),
+               lbx=lbx, ubx=ubx, lbg=lbg, ubg=ubg)
+    return out
+
+
+def generate(args):
+    name, solver, K = args
+    t0 = time.time()
+    out = run(name, solver, K)
+    suffix = "" if solver == "numpy" else f"_{solver}"
+    path = os.path.join(HERE, f"ref_run_{name}{suffix}.npz")
+    np.savez_compressed(path, **out)
+    st = out["status"]
+    print(f"{name} ({solver}): {len(st)} steps in {time.time() - t0:.0f}s; statuses "
+          f"{dict(zip(*np.unique(st, return_counts=True)))}; mean iter {out['iter'].mean():.2f}; "
+          f"FOV-error sum {out['fov_sum']:.6f}", flush=True)
+    return path
+
+
+if __name__ == "__main__":
+    ap = argparse.ArgumentParser()
+    ap.add_argument("run", nargs="?", default="all")
+    ap.add_argument("--solver", choices=["numpy", "cpp"], default="numpy")
+    ap.add_argument("--steps", type=int, default=0, help="override the run length (0: the script's)")
+    a = ap.parse_args()
+    names = list(RUNS) if a.run == "all" else [a.run]
+    jobs = [(n, a.solver, a.steps or None) for n in names]
+    if len(jobs) == 1:
+        generate(jobs[0])
+    else:
+        with mp.get_context("fork").Pool(len(jobs)) as pool:
+            pool.map(generate, jobs)

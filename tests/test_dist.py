@@ -34,6 +34,36 @@ def _solve_rows(P, spec):
     return np.array(rows)
 
 
+def _worker_uneven(rank, world, port, total, q):
+    """Rows tagged with their global scenario index, sharded unevenly (total % world != 0)."""
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(root, "mpc-implementation_amd"))
+    from nmpc_amd.dist import shard, gather_rows, gather_closed_loop
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    sl = shard(total, world, rank)
+    idx = torch.arange(sl.start, sl.stop, dtype=torch.float64)
+    local = torch.stack([idx, idx * 10 + 1, -idx], dim=1)
+    allr = gather_rows(local, world, total=total)
+    # the fused closed loop's packed histories (K steps of u0, f, status) over the same shards
+    K, B = 3, sl.stop - sl.start
+    hist = {"u": idx[None, :, None].repeat(K, 1, 6) + torch.arange(K, dtype=torch.float64)[:, None, None],
+            "f": idx[None, :].repeat(K, 1) * 2, "status": torch.zeros(K, B, dtype=torch.int32)}
+    cl = gather_closed_loop(hist, world, total=total)
+    try:
+        # a block that is not this rank's shard is refused (on every rank, before any collective)
+        gather_rows(torch.cat([local, torch.zeros(1, 3, dtype=local.dtype)]), world, total=total)
+        bad = False
+    except ValueError:
+        bad = True
+    if rank == 0:
+        q.put((allr.numpy(), cl.numpy(), bad))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
 def _worker(rank, world, port, total, q):
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -85,3 +115,26 @@ def test_gloo_world2_gather_matches_serial():
     spec = make_spec("race_track_2", N=5, T=0.2)
     want = _solve_rows(draw_scenarios(spec, total, seed=99), spec)
     np.testing.assert_array_equal(got, want)
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("total,world", [(10, 3), (7, 3), (2, 3)])
+def test_gloo_world3_uneven_shards_gather(total, world):
+    """total % world != 0: shard() gives unequal blocks; the gather pads to the largest
+    block and returns exactly the global rows in order (bench.py's fused-mode exchange)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_uneven, args=(r, world, port, total, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    allr, cl, bad = q.get(timeout=240)
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    idx = np.arange(total, dtype=np.float64)
+    np.testing.assert_array_equal(allr, np.stack([idx, idx * 10 + 1, -idx], axis=1))
+    assert cl.shape == (total, 8 * 3)
+    np.testing.assert_array_equal(cl[:, 0], idx)            # step 0's u0[0] = scenario index
+    np.testing.assert_array_equal(cl[:, 6 * 3], idx * 2)    # step 0's f
+    assert bad

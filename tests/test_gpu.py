@@ -721,7 +721,8 @@ def test_step_queue_guard_reports_unrun_scenarios():
     s.closed_loop_device(1, *bnd, torch.tensor(P0, **f64), torch.zeros(8, spec.nw, **f64), vt0, wt0)
     B, K = s.closed_loop_info()["resident_waves"] + 64, 2
     P, bnd, vt, wt = _closed_loop_inputs(spec, B, 11)
-    hist = {"u": torch.zeros(K, B, 6, **f64), "f": torch.zeros(K, B, **f64),
+    hist = {"u": torch.zeros(K, B, 6, **f64), "f": torch.zeros(K, B, **f64), "x": torch.zeros(K, B, 8, **f64),
+            "fov": torch.zeros(K, B, **f64), "iters": torch.full((K, B), 99, dtype=torch.int32, device="cuda"),
             "status": torch.full((K, B), 99, dtype=torch.int32, device="cuda")}
     os.environ["NMPC_SCHED_TEST_ONE_SET"] = "1"
     try:
@@ -736,7 +737,50 @@ def test_step_queue_guard_reports_unrun_scenarios():
     assert np.all(st[:, pos % 8 != 0] == NOT_RUN)
     assert np.all(st[:, pos % 8 == 0] != NOT_RUN) and np.all(st != 99)
     assert np.isnan(hist["f"].cpu().numpy()[:, pos % 8 != 0]).all()
+    # every history of an unrun step is marked, none is left uninitialised
+    assert np.isnan(hist["fov"].cpu().numpy()[:, pos % 8 != 0]).all()
+    assert np.isnan(hist["x"].cpu().numpy()[:, pos % 8 != 0]).all()
+    assert np.isnan(hist["u"].cpu().numpy()[:, pos % 8 != 0]).all()
+    assert np.all(hist["iters"].cpu().numpy()[:, pos % 8 != 0] == NOT_RUN)
     assert info["steps_done"] == K * int((pos % 8 == 0).sum())
+
+
+@pytest.mark.parametrize("policy", ["step_queues", "static"])
+def test_closed_loop_check_on_a_side_stream(policy):
+    """check=True on a non-blocking torch stream: nmpc_closed_loop_info synchronises the
+    launch's own stream before reading the completion flags, so the check sees this
+    launch (not the previous one) under both policies; the one-workgroup-per-scenario
+    policy is counted by the same check kernel."""
+    import torch
+    from nmpc_amd import make_spec
+
+    spec = make_spec("race_track_2", N=6, T=0.2)
+    s = _solver(spec)
+    f64 = dict(dtype=torch.float64, device="cuda")
+    P0, bnd, vt0, wt0 = _closed_loop_inputs(spec, 8, 5)
+    s.closed_loop_device(1, *bnd, torch.tensor(P0, **f64), torch.zeros(8, spec.nw, **f64), vt0, wt0)
+    B = s.closed_loop_info()["resident_waves"] + 64 if policy == "step_queues" else 96
+    K = 3
+    P, bnd, vt, wt = _closed_loop_inputs(spec, B, 21)
+    res = []
+    for use_side in (False, True):
+        hist = {"status": torch.full((K, B), 99, dtype=torch.int32, device="cuda")}
+        p, w = torch.tensor(P, **f64), torch.zeros(B, spec.nw, **f64)
+        torch.cuda.synchronize()
+        if use_side:
+            st = torch.cuda.Stream()
+            with torch.cuda.stream(st):
+                s.closed_loop_device(K, *bnd, p, w, vt, wt, hist, stream=st, check=True)
+            st.synchronize()
+        else:
+            s.closed_loop_device(K, *bnd, p, w, vt, wt, hist, check=True)
+        info = s.closed_loop_info()
+        assert info["policy"] == policy and info["steps_done"] == B * K and info["scheduler_error"] == 0
+        res.append(hist["status"].cpu().numpy())
+    np.testing.assert_array_equal(res[0], res[1])
+    with pytest.raises(ValueError, match="permutation"):
+        order = torch.zeros(B, dtype=torch.int32, device="cuda")  # every entry the same scenario
+        s.closed_loop_device(K, *bnd, torch.tensor(P, **f64), torch.zeros(B, spec.nw, **f64), vt, wt, order=order)
 
 
 @pytest.mark.parametrize("layout,N,dyn,model,weights", [("race_track_2", 12, False, "uav8g", False),

@@ -11,7 +11,9 @@ Two comparisons per case:
     the north-star tolerance |a - b| <= 1e-6 (1 + |b|);
   * chained: nmpc_closed_loop_dev from the fixture's start, compared step by step
     (status, u0, f) until the two loops first disagree.
-Mismatches are printed; the thresholds below are what the test enforces.
+Every mismatch is printed.  The thresholds are the measured agreement of the current
+kernel minus at most one scenario or step of slack, so a
+regression that breaks even one scenario in a few hundred fails loudly.
 """
 import os
 
@@ -59,18 +61,25 @@ def _per_step(name):
     print(f"\n{name} per step: {len(ost)} solves; status agree {same.mean():.4f}; iterations agree "
           f"{(it == oit).mean():.4f}; converged+agreeing {conv.sum()}, within 1e-6 {ok_x.sum()}; "
           f"oracle statuses {dict(zip(*np.unique(ost, return_counts=True)))}")
-    for i in np.flatnonzero(~same | (conv & ~ok_x))[:12]:
+    for i in np.flatnonzero(~same | (conv & ~ok_x) | (it != oit)):
         print(f"  step {i}: gpu status {st[i]} it {it[i]} | oracle status {ost[i]} it {oit[i]} | "
               f"x rel err {ex[i]:.2e} f rel err {ef[i]:.2e}")
     return same, conv, ok_x, it == oit
 
 
+# measured (round 2/3 kernels): statuses 318/320, 320/320, 1280/1280, 160/160; iterations
+# 1277/1280 (config 3), 160/160 (config 5); every converged agreeing step within 1e-6
+PER_STEP_MIN = {"config1": (318, 314), "config2": (320, 318), "config3": (1280, 1276), "config5": (160, 159)}
+CHAIN_MIN = {"config1": 31, "config2": 32, "config3": 63, "config5": 14}  # identical chains (of 32/32/64/16)
+
+
 @pytest.mark.parametrize("name", ["config1", "config2", "config3", "config5"])
 def test_per_step_parity_with_oracle_fixture(name):
     same, conv, ok_x, same_it = _per_step(name)
-    assert same.mean() >= 0.95
-    assert ok_x.sum() >= 0.95 * conv.sum()
-    assert same_it.mean() >= 0.90
+    smin, imin = PER_STEP_MIN[name]
+    assert same.sum() >= smin
+    assert ok_x.sum() == conv.sum()
+    assert same_it.sum() >= imin
 
 
 def test_config5_cold_solves_match_oracle():
@@ -85,7 +94,7 @@ def test_config5_cold_solves_match_oracle():
     print(f"\nconfig5 cold: gpu {dict(zip(*np.unique(st, return_counts=True)))} "
           f"oracle {dict(zip(*np.unique(z['cold_status'], return_counts=True)))}; "
           f"iterations agree {(it == z['cold_iter']).mean():.3f}")
-    assert (st == z["cold_status"]).mean() >= 15 / 16
+    assert (st == z["cold_status"]).sum() >= 15
     conv = (st == z["cold_status"]) & np.isin(st, (0, 1))
     if conv.any():
         assert np.all(_relerr(sol["x"].T[conv], z["cold_x"][conv]) <= TOL)
@@ -133,10 +142,9 @@ def test_chained_closed_loop_matches_oracle_fixture(name):
           f"the first divergence")
     # the device loop's shift (fused multiply-adds) and numpy's differ by rounding; near a
     # termination threshold that can change an iteration count and the chain from there
-    # on, so chains are required to agree up to their first divergence on 90% of the
-    # steps (the per-step test above compares every step from identical inputs)
-    assert matched >= 0.9 * total
-    assert full >= 0.75 * B
+    # on (the per-step test above compares every step from identical inputs)
+    assert full >= CHAIN_MIN[name]
+    assert matched >= total - (B - CHAIN_MIN[name]) * K
 
 
 def test_config3_closed_loop_at_bench_scale_matches_cpu_restatement():
@@ -182,15 +190,17 @@ def test_config3_closed_loop_at_bench_scale_matches_cpu_restatement():
                 if ok:
                     worst = max(worst, eu, ef)
             if not ok:
+                print(f"  scenario {b} parts at step {k}: gpu status {gs[b, k]} | cpu status {rs[b, k]}")
                 chain = False
                 break
             matched += 1
         full += chain
     print(f"\nconfig 3 at bench scale: status agreement {agree:.4f} over {B * K} steps; {full}/{B} chains "
           f"identical; {matched} steps before the first divergence; max rel err {worst:.2e}")
-    assert agree >= 0.99
-    assert full >= 0.9 * B
-    assert matched >= 0.95 * B * K
+    # measured: agreement 0.995, 3,865-3,877 identical chains, 79,987-80,112 steps
+    assert agree >= 0.994
+    assert full >= 3860
+    assert matched >= 79900
 
 
 def test_config3_fov_error_sums_match_oracle():
@@ -281,6 +291,7 @@ def test_config5_closed_loop_sample_matches_cpu_restatement():
                 ok = (np.max(np.abs(H["u"][k, b] - ref["u0"][b, k]) / (1 + np.abs(ref["u0"][b, k]))) <= TOL and
                       abs(H["f"][k, b] - ref["f"][b, k]) <= TOL * (1 + abs(ref["f"][b, k])))
             if not ok:
+                print(f"  scenario {b} parts at step {k}: gpu status {gs[b, k]} | cpu status {rs[b, k]}")
                 chain = False
                 break
             matched += 1
@@ -291,6 +302,6 @@ def test_config5_closed_loop_sample_matches_cpu_restatement():
     # a max_iter step (a fifth of them here) returns an unconverged iterate, which the
     # next step starts from: chains can part at rounding level there (last run: status
     # agreement 0.9955, 885/1024 chains identical, 4682/5120 steps before divergence)
-    assert agree >= 0.98
-    assert full >= 0.75 * B
-    assert matched >= 0.85 * B * K
+    assert agree >= 0.995
+    assert full >= 880
+    assert matched >= 4670
