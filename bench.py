@@ -117,6 +117,21 @@ def cpu_baseline(spec_cfg, cfg, P, lbx, ubx, lbg, ubg, K, budget_s=15.0):
     cpu_baseline.sample_rows = int(rows.max()) + 1 if len(rows) else 0
     its = np.concatenate([r["iter"][b, :done[b]] for b in rows]) if len(rows) else np.zeros(0)
     sts = np.concatenate([r["status"][b, :done[b]] for b in rows]) if len(rows) else np.zeros(0, int)
+    tsv = np.concatenate([r["solve_s"][b, :done[b]] for b in rows]) if len(rows) else np.zeros(0)
+    # cold-start leg (cold u = 0 and warm-started): every scenario's first
+    # NLP from u = 0, the same threads
+    t1 = time.perf_counter()
+    rc = cpu_ipopt.solve_batch(prob, np.zeros((P.shape[0], spec_cfg.nw)), P, lbx, ubx, lbg, ubg,
+                               orc.REFERENCE_OPTS, threads=nthr)
+    cwall = time.perf_counter() - t1
+
+    def pct(v):
+        return {"p50_ms": float(np.percentile(v, 50) * 1e3), "p99_ms": float(np.percentile(v, 99) * 1e3),
+                "max_ms": float(v.max() * 1e3)} if len(v) else None
+    cold = {"value": P.shape[0] / cwall, "unit": "NLP solves/s", "solves": int(P.shape[0]), "wall_s": cwall,
+            "mean_ip_iterations": float(rc["iter"].mean()), "per_solve_wall": pct(rc["solve_s"]),
+            "status_histogram": {int(k): int(v) for k, v in zip(*np.unique(rc["status"], return_counts=True))},
+            "sample": f"cold solves (u = 0) of all {P.shape[0]} bench scenarios, {nthr} threads"}
     return {"value": n / wall, "unit": "MPC steps/s", "cores": nthr, "kind": "port",
             "sample": f"{n} warm-started closed-loop MPC steps (solve + shift, up to {K} per scenario, "
                       f"{len(rows)} of the bench's config-{cfg} scenarios) by oracle/cpu_ipopt.cpp (CPU "
@@ -124,7 +139,9 @@ def cpu_baseline(spec_cfg, cfg, P, lbx, ubx, lbg, ubg, K, budget_s=15.0):
                       f"{nthr} threads, budget {budget_s:.0f}s, wall {wall:.1f}s",
             "mean_ip_iterations": float(its.mean()) if n else None,
             "iterations_per_s_per_core": float(its.sum() / wall / nthr) if n else None,
-            "status_histogram": {int(k): int(v) for k, v in zip(*np.unique(sts, return_counts=True))}}
+            "per_solve_wall": pct(tsv),
+            "status_histogram": {int(k): int(v) for k, v in zip(*np.unique(sts, return_counts=True))},
+            "cold_start": cold}
 
 
 def parity_sample(solver, spec, P, K, records, bnd, dev, tol=1e-6):
@@ -192,12 +209,15 @@ def main():
     ap.add_argument("--in-order", action="store_true",
                     help="fused mode: dispatch scenarios in index order (no longest-first order)")
     ap.add_argument("--cpu-budget", type=float, default=20.0)
+    ap.add_argument("--dump-rows", default="",
+                    help="fused mode: rank 0 saves the gathered (scenarios, 8K) per-step rows (u0, f, status) "
+                         "of the timed launch to this .npy (multi-rank rehearsal test)")
     args = ap.parse_args()
 
     import torch
     import torch.distributed as dist
     from nmpc_amd import nlpsol, config_spec, draw_scenarios, REFERENCE_OPTS
-    from nmpc_amd.dist import shard, pack_result, gather_rows, gather_closed_loop
+    from nmpc_amd.dist import shard, pack_result, gather_rows, gather_closed_loop, pack_closed_loop
     from nmpc_amd.schedule import longest_first
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -244,6 +264,12 @@ def main():
     v_t = torch.full((B,), 12.0, **f64)   # target speed, Python/NMPC_TT.py:25
     w_t = torch.full((B,), 0.01, **f64)   # target turn rate
     stream = torch.cuda.current_stream()
+    # moving obstacles (config 5: MATLAB/Dynamic Obstacles/Dynamic Obstacle avoidance.m:213-230,
+    # from MPC iteration 195 as in the config-5 fixtures; the W warm-up steps come first)
+    pstep = None
+    if spec.np > spec.np_min:
+        from nmpc_amd.targets import obstacle_steps
+        pstep = torch.tensor(obstacle_steps(195, W + K, spec.np), **f64)
 
     def hist_bufs(k):
         return {"u": torch.empty(k, B, 6, **f64), "f": torch.empty(k, B, **f64), "fov": torch.zeros(k, B, **f64),
@@ -252,7 +278,7 @@ def main():
     out = {"x": torch.empty(B, spec.nw, **f64), "f": torch.empty(B, **f64),
            "status": torch.empty(B, **i32), "iters": torch.empty(B, **i32)}
 
-    def per_step(p, w, hist, k, cold, timed_events=None):
+    def per_step(p, w, hist, k, cold, timed_events=None, g=None):
         """One batched step: solve launch (+ shift launch) (+ per-step gather)."""
         if timed_events is not None:
             timed_events[0].record(stream)
@@ -261,6 +287,8 @@ def main():
             timed_events[1].record(stream)
         if not cold:
             solver.shift_device(p, out["x"], w, v_t, w_t, stream=stream)
+            if pstep is not None:  # obstacle coordinates move after the step (nmpc_closed_loop_dev's p_step)
+                p[:, spec.np_min:] += pstep[k if g is None else g, spec.np_min:]
         if world > 1:  # per-step gather of (u0, f, status)
             gather_rows(pack_result(out["x"], out["f"], out["status"], spec.nu), world, total=B * world)
         hist["u"][k].zero_(); hist["u"][k][:, :spec.nu].copy_(out["x"][:, :spec.nu]); hist["f"][k].copy_(out["f"])
@@ -269,11 +297,16 @@ def main():
     def fused(p, w, hist, k_steps, timed_events=None, order=None):
         if timed_events is not None:
             timed_events[0].record(stream)
-        solver.closed_loop_device(k_steps, *bnd, p, w, v_t, w_t, hist, stream=stream, order=order, check=False)
+        solver.closed_loop_device(k_steps, *bnd, p, w, v_t, w_t, hist, stream=stream, order=order, check=False,
+                                  p_step=None if pstep is None else pstep[W:W + k_steps].contiguous())
         if timed_events is not None:
             timed_events[1].record(stream)
         if world > 1:  # the only exchange: final gather of every step's (u0, f, status)
-            gather_closed_loop(hist, world, total=B * world)
+            rows = gather_closed_loop(hist, world, total=B * world)
+        else:
+            rows = pack_closed_loop(hist) if args.dump_rows else None
+        if timed_events is not None:
+            fused.rows = rows
 
     def barrier_sync():
         torch.cuda.synchronize()
@@ -304,7 +337,7 @@ def main():
             fused(p, w, ht, K, evs[0], order=order)
         else:
             for k in range(K):
-                per_step(p, w, ht, k, mode == "cold", evs[k])
+                per_step(p, w, ht, k, mode == "cold", evs[k], g=W + k)
         barrier_sync()
         elapsed = time.perf_counter() - t0
         if mode == "fused":  # every (scenario, step) ran: raises otherwise (after the timed region)
@@ -418,6 +451,8 @@ def main():
                 res["parity_sample"] = parity_sample(solver, spec, P_all[:cpu_baseline.sample_rows], K,
                                                      cpu_baseline.records, bnd, dev)
         print(json.dumps(res))
+        if args.dump_rows and args.mode == "fused":
+            np.save(args.dump_rows, fused.rows.cpu().numpy())
     if world > 1:
         dist.destroy_process_group()
 

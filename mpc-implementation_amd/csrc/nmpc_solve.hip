@@ -106,6 +106,9 @@ constexpr Lay make_layout(int N, int m, bool lr, bool refine) {
   if (!lr) {
     L.s = g; g += al8(ng); L.y = g; g += al8(ng); L.vl = g; g += al8(ng); L.vu = g; g += al8(ng);
     L.d = g; g += al8(ng); L.ds = g; g += al8(ng); L.ds2 = g; g += al8(ng); L.dc = g; g += al8(ng);
+    // the row bounds go with the rows: in the workspace for the global-row classes, whose
+    // LDS then holds only per-stage data (config 5's N = 50 class fits 5 scenarios per CU)
+    L.dl = g; g += al8(ng); L.du = g; g += al8(ng);
   }
   // trial row values: in LDS with the hot rows (not in the refinement classes, whose
   // LDS budget holds the refinement's step instead)
@@ -142,7 +145,7 @@ constexpr Lay make_layout(int N, int m, bool lr, bool refine) {
 #else
   L.red = o;
 #endif
-  L.dl = o; o += al2(ng); L.du = o; o += al2(ng);  // row bounds (constant during a solve, read by every row pass)
+  if (lr) { L.dl = o; o += al2(ng); L.du = o; o += al2(ng); }  // row bounds (constant during a solve, read by every row pass)
   L.rvars = o; o += 48;  // line-search / restoration scalars; [32..36] barrier sums; [40..45] watchdog; [46] #fixed
   L.fixm = o; o += al2(N / 2 + 1);  // fixed-control masks, one int per stage
   L.rdX = o; if (refine) o += al2(nX);  // refinement step in X (fp32 classes)
@@ -361,7 +364,8 @@ struct Solver {
   GLB double *wU, *wzl, *wzu, *wdU, *wsl, *wy, *wvl, *wvu, *wds, *wpR, *wnR, *wzpR, *wznR, *wdpR, *wdnR, *wdyR;
   double rho, etaR;  // restoration: penalty, proximity weight * sqrt(mu)
   double* wsbase;    // workspace base of all scenarios (restoration re-binds from it)
-  LDS double *dl, *du, *rvars;
+  RV *dl, *du;  // row bounds: LDS or global with the rows (Cap::lds_rows)
+  LDS double* rvars;
   GLB double* gl, *Hl, *Qs;
   LDS double* trig, *qs, *lam;
   GLB double* K, *Rk;
@@ -397,7 +401,7 @@ struct Solver {
     d = rvp(L.d); ds = rvp(L.ds); ds2 = rvp(L.ds2);
     if constexpr (CAP::lds_rows && !CAP::refine) dt = (DTT*)(sm + L.dt);
     else dt = (DTT*)(gw + L.dt);
-    dc = rvp(L.dc); dl = sm + L.dl; du = sm + L.du; dms = gw + L.dms; rvars = sm + L.rvars;
+    dc = rvp(L.dc); dl = rvp(L.dl); du = rvp(L.du); dms = gw + L.dms; rvars = sm + L.rvars;
     UR = gw + L.UR; zl0 = gw + L.zl0; zu0 = gw + L.zu0; s0 = gw + L.s0; vl0 = gw + L.vl0; vu0 = gw + L.vu0;
     pR = gw + L.pR; nR = gw + L.nR; zpR = gw + L.zpR; znR = gw + L.znR; dpR = gw + L.dpR; dnR = gw + L.dnR;
     dyR = gw + L.dyR; dp2R = gw + L.dp2R; dn2R = gw + L.dn2R; dy2R = gw + L.dy2R; cms = gw + L.cms;
@@ -3548,10 +3552,15 @@ ClassFns nmpc_class_fns_B();
 ClassFns nmpc_class_fns_C();
 ClassFns nmpc_class_fns_A32();
 ClassFns nmpc_class_fns_C32();
+ClassFns nmpc_class_fns_D();
 
 using CapA = Cap<20, 15, true>;   // BASELINE configs 2-4 (N=20, <=10 obstacles) and the reference's N=15 scripts
 using CapB = Cap<31, 21>;
 using CapC = Cap<63, 21>;   // any supported shape
+// BASELINE config 5 (N = 50, 10 obstacles): global rows and row bounds, 29 KB of LDS per
+// scenario, so 5 scenarios per CU (class C's 36 KB allows 4; before the row bounds left
+// LDS, 57 KB allowed 2)
+using CapD = Cap<50, 15>;
 // fp32 Riccati factorisation (nmpc_options.linear_solver_fp32; BASELINE config 5's fp32 leg)
 using CapA32 = Cap<20, 15, true, float>;
 using CapC32 = Cap<63, 21, false, float>;
@@ -3570,8 +3579,10 @@ ClassFns nmpc_class_fns_B() { return class_fns<CapB>(); }
 ClassFns nmpc_class_fns_C() { return class_fns<CapC>(); }
 #elif NMPC_TU_CLASS == 4
 ClassFns nmpc_class_fns_A32() { return class_fns<CapA32>(); }
-#else
+#elif NMPC_TU_CLASS == 5
 ClassFns nmpc_class_fns_C32() { return class_fns<CapC32>(); }
+#else
+ClassFns nmpc_class_fns_D() { return class_fns<CapD>(); }
 #endif
 #else  // host translation unit
 
@@ -3617,11 +3628,13 @@ static void pick_class(const Params& P, KernFn* fn, LoopFn* lfn, SchedFn* sfn, i
   if (P.o.linear_solver_fp32) c = fit_a ? nmpc_class_fns_A32() : nmpc_class_fns_C32();
   else if (fit_a) c = nmpc_class_fns_A();
   else if (P.N <= CapB::nmax && P.m <= CapB::mmax) c = nmpc_class_fns_B();
+  else if (P.N <= CapD::nmax && P.m <= CapD::mmax) c = nmpc_class_fns_D();
   else c = nmpc_class_fns_C();
   // diagnostics: run a fitting problem on a larger class (global row vectors)
   if (const char* e = std::getenv("NMPC_FORCE_CLASS")) {
     if (e[0] == 'B' && P.N <= CapB::nmax && P.m <= CapB::mmax && !P.o.linear_solver_fp32) c = nmpc_class_fns_B();
     if (e[0] == 'C' && !P.o.linear_solver_fp32) c = nmpc_class_fns_C();
+    if (e[0] == 'D' && P.N <= CapD::nmax && P.m <= CapD::mmax && !P.o.linear_solver_fp32) c = nmpc_class_fns_D();
   }
   *fn = c.fn; *lfn = c.lfn; *sfn = c.sfn; *lds_doubles = c.lds_doubles; *ws_doubles = c.ws_doubles;
 }

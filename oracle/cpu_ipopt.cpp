@@ -2094,7 +2094,7 @@ const char* nmpc_cpu_option_names() {
 int nmpc_cpu_solve_batch(const nmpc_cpu_problem* prob, const double* opts, int64_t B, const double* w0,
                          const double* p, const double* lbx, const double* ubx, const double* lbg, const double* ubg,
                          double* x_out, double* f_out, double* g_out, double* lam_x_out, double* lam_g_out,
-                         int32_t* status_out, int32_t* iter_out, int nthreads) {
+                         int32_t* status_out, int32_t* iter_out, int nthreads, double* solve_s) {
   if (!prob || !opts || B < 0) return 1;
   const Prob P = make_prob(*prob);
   const Opts o = opts_from(opts);
@@ -2105,7 +2105,9 @@ int nmpc_cpu_solve_batch(const nmpc_cpu_problem* prob, const double* opts, int64
     Result R;
 #pragma omp for schedule(dynamic, 1)
     for (int64_t b = 0; b < B; ++b) {
+      const auto ts = std::chrono::steady_clock::now();
       S.solve(w0 + b * P.n, p + b * P.np, lbx, ubx, lbg, ubg, R);
+      if (solve_s) solve_s[b] = std::chrono::duration<double>(std::chrono::steady_clock::now() - ts).count();
       std::memcpy(x_out + b * P.n, R.x.data(), sizeof(double) * P.n);
       f_out[b] = R.F;
       if (g_out) std::memcpy(g_out + b * P.m, R.g.data(), sizeof(double) * P.m);
@@ -2123,11 +2125,12 @@ int nmpc_cpu_solve_batch(const nmpc_cpu_problem* prob, const double* opts, int64
 // p[nx+3:] += p_step[k] when p_step (K x np) is given), starting from
 // p (B x np: x0, target, obstacle parameters) and w = 0.  Stops taking new steps
 // once budget_s seconds have passed (budget_s <= 0: no limit); steps_done[b] says
-// how many steps scenario b ran.  Histories: status / iter (B x K), u0 (B x K x nu), f.
+// how many steps scenario b ran.  Histories: status / iter (B x K), u0 (B x K x nu), f,
+// and (nullable) each solve's wall time in seconds (B x K).
 int nmpc_cpu_closed_loop(const nmpc_cpu_problem* prob, const double* opts, int64_t B, int32_t K, const double* p0,
                          const double* lbx, const double* ubx, const double* lbg, const double* ubg, double vt,
                          double wt, const double* p_step, double budget_s, int nthreads, int32_t* status_out, int32_t* iter_out,
-                         double* u0_out, double* f_out, int32_t* steps_done) {
+                         double* u0_out, double* f_out, int32_t* steps_done, double* solve_s) {
   if (!prob || !opts || B < 0 || K < 0) return 1;
   const Prob P = make_prob(*prob);
   const Opts o = opts_from(opts);
@@ -2146,7 +2149,9 @@ int nmpc_cpu_closed_loop(const nmpc_cpu_problem* prob, const double* opts, int64
       int k = 0;
       for (; k < K; ++k) {
         if (budget_s > 0 && elapsed() >= budget_s) break;
+        const auto ts = std::chrono::steady_clock::now();
         S.solve(w.data(), p.data(), lbx, ubx, lbg, ubg, R);
+        if (solve_s) solve_s[b * K + k] = std::chrono::duration<double>(std::chrono::steady_clock::now() - ts).count();
         status_out[b * K + k] = R.status;
         iter_out[b * K + k] = R.iter;
         f_out[b * K + k] = R.F;

@@ -44,9 +44,9 @@ def lib():
         L.nmpc_cpu_option_names.restype = C.c_char_p
         dp, ip = C.POINTER(C.c_double), C.POINTER(C.c_int32)
         L.nmpc_cpu_solve_batch.argtypes = [C.POINTER(CpuProblem), dp, C.c_int64, dp, dp, dp, dp, dp, dp,
-                                           dp, dp, dp, dp, dp, ip, ip, C.c_int]
+                                           dp, dp, dp, dp, dp, ip, ip, C.c_int, dp]
         L.nmpc_cpu_closed_loop.argtypes = [C.POINTER(CpuProblem), dp, C.c_int64, C.c_int32, dp, dp, dp, dp, dp,
-                                           C.c_double, C.c_double, dp, C.c_double, C.c_int, ip, ip, dp, dp, ip]
+                                           C.c_double, C.c_double, dp, C.c_double, C.c_int, ip, ip, dp, dp, ip, dp]
         _lib = L
     return _lib
 
@@ -93,19 +93,21 @@ def _f64(a, shape=None):
 
 def solve_batch(prob, W0, P, lbx, ubx, lbg, ubg, opts=None, threads=0):
     """B independent solves; W0 (B, nw), P (B, np).  Returns a dict like the oracle's
-    result (x, f, g, lam_x, lam_g, status, iter), batched."""
+    result (x, f, g, lam_x, lam_g, status, iter), batched, plus each solve's wall time
+    (solve_s, seconds)."""
     W0 = _f64(W0)
     P = _f64(P)
     B = W0.shape[0]
     nw, m = prob.nw, prob.ng
     out = {"x": np.empty((B, nw)), "f": np.empty(B), "g": np.empty((B, m)), "lam_x": np.empty((B, nw)),
-           "lam_g": np.empty((B, m)), "status": np.empty(B, np.int32), "iter": np.empty(B, np.int32)}
+           "lam_g": np.empty((B, m)), "status": np.empty(B, np.int32), "iter": np.empty(B, np.int32),
+           "solve_s": np.zeros(B)}
     cp = problem_struct(prob)
     oa = options_array(opts)
     bl = [_f64(b) for b in (lbx, ubx, lbg, ubg)]
     rc = lib().nmpc_cpu_solve_batch(C.byref(cp), _p(oa), B, _p(W0), _p(P), *[_p(b) for b in bl], _p(out["x"]),
                                     _p(out["f"]), _p(out["g"]), _p(out["lam_x"]), _p(out["lam_g"]),
-                                    _i(out["status"]), _i(out["iter"]), int(threads))
+                                    _i(out["status"]), _i(out["iter"]), int(threads), _p(out["solve_s"]))
     if rc != 0:
         raise RuntimeError(f"nmpc_cpu_solve_batch failed ({rc})")
     return out
@@ -116,18 +118,20 @@ def closed_loop(prob, P0, K, lbx, ubx, lbg, ubg, opts=None, vt=12.0, wt=0.01, p_
     """K warm-started MPC steps per scenario (solve + shift_timestep; obstacle
     parameters advanced by p_step[k] (K, np) after step k), from p0 rows and w = 0.
     Stops starting new steps after budget_s seconds (0: no limit).  Returns status /
-    iter (B, K), u0 (B, K, nu), f (B, K), steps (B,)."""
+    iter (B, K), u0 (B, K, nu), f (B, K), steps (B,), and solve_s (B, K): each solve's
+    wall time in seconds."""
     P0 = _f64(P0)
     ps = None if p_step is None else _f64(p_step, (K, prob.np_))
     B = P0.shape[0]
     out = {"status": np.full((B, K), -1000, np.int32), "iter": np.zeros((B, K), np.int32),
-           "u0": np.full((B, K, prob.nu), np.nan), "f": np.full((B, K), np.nan), "steps": np.zeros(B, np.int32)}
+           "u0": np.full((B, K, prob.nu), np.nan), "f": np.full((B, K), np.nan), "steps": np.zeros(B, np.int32),
+           "solve_s": np.full((B, K), np.nan)}
     cp = problem_struct(prob)
     oa = options_array(opts)
     bl = [_f64(b) for b in (lbx, ubx, lbg, ubg)]
     rc = lib().nmpc_cpu_closed_loop(C.byref(cp), _p(oa), B, int(K), _p(P0), *[_p(b) for b in bl], float(vt),
                                     float(wt), None if ps is None else _p(ps), float(budget_s), int(threads), _i(out["status"]), _i(out["iter"]),
-                                    _p(out["u0"]), _p(out["f"]), _i(out["steps"]))
+                                    _p(out["u0"]), _p(out["f"]), _i(out["steps"]), _p(out["solve_s"]))
     if rc != 0:
         raise RuntimeError(f"nmpc_cpu_closed_loop failed ({rc})")
     return out

@@ -351,13 +351,13 @@ def test_closed_loop_dispatch_order_does_not_change_results():
     f64 = dict(dtype=torch.float64, device="cuda")
     s = _solver(spec)
 
-    def run(order):
+    def run(order, validate=True):
         p = torch.tensor(P, **f64)
         w = torch.zeros(B, spec.nw, **f64)
         hist = {"u": torch.empty(K, B, 6, **f64), "f": torch.empty(K, B, **f64),
                 "status": torch.full((K, B), 99, dtype=torch.int32, device="cuda"),
                 "iters": torch.full((K, B), -1, dtype=torch.int32, device="cuda")}
-        s.closed_loop_device(K, *bnd, p, w, vt, wt, hist, order=order)
+        s.closed_loop_device(K, *bnd, p, w, vt, wt, hist, order=order, check=validate, _validate_order=validate)
         torch.cuda.synchronize()
         return {k: v.cpu().numpy() for k, v in hist.items()}, p.cpu().numpy(), w.cpu().numpy()
 
@@ -370,13 +370,20 @@ def test_closed_loop_dispatch_order_does_not_change_results():
             np.testing.assert_array_equal(got[k], ref[k], err_msg=k)
         np.testing.assert_array_equal(p_got, p_ref)
         np.testing.assert_array_equal(w_got, w_ref)
-    # out-of-range entries: those workgroups do nothing, the named scenarios still run
+    # out-of-range entries (not a permutation: nlpsol refuses it; here handed to the device
+    # directly): those workgroups do nothing, the named scenarios still run, and the
+    # completion guard marks the two scenarios left unrun and reports the launch
+    from nmpc_amd.nlpsol import NOT_RUN
     bad = torch.arange(B, dtype=torch.int32, device="cuda")
     bad[1] = B + 7
     bad[2] = -3
-    got, _, _ = run(bad)
-    assert (got["iters"][:, 1] == -1).all() and (got["iters"][:, 2] == -1).all()
+    with pytest.raises(ValueError, match="permutation"):
+        run(bad)
+    got, _, _ = run(bad, validate=False)
+    assert (got["iters"][:, 1:3] == NOT_RUN).all() and (got["status"][:, 1:3] == NOT_RUN).all()
     np.testing.assert_array_equal(got["iters"][:, 3:], ref["iters"][:, 3:])
+    info = s.closed_loop_info()
+    assert info["scheduler_error"] & 2 and info["steps_done"] == (B - 2) * K
 
 
 def test_closed_loop_step_queues_match_per_scenario_dispatch():
@@ -745,7 +752,7 @@ def test_step_queue_guard_reports_unrun_scenarios():
     assert info["steps_done"] == K * int((pos % 8 == 0).sum())
 
 
-@pytest.mark.parametrize("policy", ["step_queues", "static"])
+@pytest.mark.parametrize("policy", ["step_queues", "per_scenario"])
 def test_closed_loop_check_on_a_side_stream(policy):
     """check=True on a non-blocking torch stream: nmpc_closed_loop_info synchronises the
     launch's own stream before reading the completion flags, so the check sees this

@@ -244,7 +244,7 @@ def test_config3_fov_error_sums_match_oracle():
         compared += 1
     print(f"\nFOV-error sums over {K} steps: {compared}/{B} scenarios compared; total {tot_g:.6f} (GPU) vs "
           f"{tot_o:.6f} (oracle); max per-scenario rel. difference {worst:.2e}")
-    assert compared >= 0.75 * B
+    assert compared >= 54  # measured 55 / 64 (the others have a max_iter / infeasible step)
     assert worst <= 1e-6
 
 

@@ -33,8 +33,11 @@ sys.path.insert(0, GOLD)
 
 # measured agreement, minus at most one step of slack
 PER_STEP_MIN = {  # (status agreement, iteration agreement, converged x outside 1e-6) in steps
-    "nmpc_tt": (693, 665, 20), "10_obstacles": (1579, 1515, 10), "race_track_2": (1980, 1900, 10)}
-CHAIN_MIN = {"nmpc_tt": 8, "10_obstacles": 40, "race_track_2": 40}
+    # measured: 699 / 685 / 11 (nmpc_tt), 1595 / 1559 / 2 (10_obstacles), 1995 / 1965 / 1 (race_track_2)
+    "nmpc_tt": (698, 684, 12), "10_obstacles": (1594, 1558, 3), "race_track_2": (1994, 1964, 2)}
+# measured agreeing prefixes 22 / 98 / 99 steps, each ended by a max_iter step whose unconverged
+# iterate parts at rounding level (the compiled restatement parts from the oracle at 8 / 102 / 111)
+CHAIN_MIN = {"nmpc_tt": 21, "10_obstacles": 97, "race_track_2": 98}
 
 
 def _load(name):
@@ -117,15 +120,17 @@ def test_reference_run_chained_and_fov_sum(name):
                          torch.tensor(wt[:, None], **f64).contiguous(), hist)
     torch.cuda.synchronize()
     H = {k: v.cpu().numpy()[:, 0] for k, v in hist.items()}
-    n = 0  # agreeing prefix: same state in, same status, converged steps' u0 / f within 1e-6
+    # agreeing prefix: every step so far had the same state in (x0 within 1e-6), the same
+    # status, and u0 and f within 1e-6 -- unconverged (max_iter) steps included: their
+    # returned iterate must agree too, or the FOV errors of the prefix could not
+    n = 0
+    eu = ex = ef = 0.0
     for k in range(K):
-        xin = z["p"][k, :8]
-        ok = (np.max(np.abs(H["x"][k] - xin) / (1 + np.abs(xin))) <= TOL and H["status"][k] == z["status"][k])
-        if ok and z["status"][k] in (0, 1):
-            ou = z["x"][k, :6]
-            ok = (np.max(np.abs(H["u"][k] - ou) / (1 + np.abs(ou))) <= TOL and
-                  abs(H["f"][k] - z["f"][k]) <= TOL * (1 + abs(z["f"][k])))
-        if not ok:
+        xin, ou = z["p"][k, :8], z["x"][k, :6]
+        ex = np.max(np.abs(H["x"][k] - xin) / (1 + np.abs(xin)))
+        eu = np.max(np.abs(H["u"][k] - ou) / (1 + np.abs(ou)))
+        ef = abs(H["f"][k] - z["f"][k]) / (1 + abs(z["f"][k]))
+        if not (ex <= TOL and H["status"][k] == z["status"][k] and eu <= TOL and ef <= TOL):
             break
         n += 1
     fg, fo = float(H["fov"][:n].sum()), float(z["fov"][:n].sum())
@@ -136,7 +141,7 @@ def test_reference_run_chained_and_fov_sum(name):
           f"{H['iters'].mean():.2f} vs {z['iter'].mean():.2f}")
     if n < K:
         print(f"  step {n}: gpu status {H['status'][n]} it {H['iters'][n]} | oracle status {z['status'][n]} "
-              f"it {z['iter'][n]}")
+              f"it {z['iter'][n]} | x0 rel err {ex:.2e}, u0 {eu:.2e}, f {ef:.2e}")
     assert n >= CHAIN_MIN[name]
     assert abs(fg - fo) <= TOL * (1 + abs(fo))
     assert np.all(np.isfinite(H["fov"])) and np.all(H["status"] != -1000)
