@@ -4,7 +4,7 @@ OUT=$1; shift
 LICM="-mllvm -disable-machine-licm"
 EXTRA=""
 for a in "$@"; do if [ "$a" == "NOLICM" ]; then LICM=""; else EXTRA="$EXTRA $a"; fi; done
-SRC=/root/repo/mpc-implementation_amd/csrc/nmpc_solve.hip
+SRC=${NMPC_SRC:-/root/repo/mpc-implementation_amd/csrc/nmpc_solve.hip}
 T=$(mktemp -d)
 F="--offload-arch=gfx950 -O3 -std=c++17 -fPIC $LICM -Wno-unused-result -Wno-unused-value $EXTRA -I /root/repo/include"
 pids=""
