@@ -84,7 +84,7 @@ struct Lay {
   // LDS
   int X, Xt, dX;
   int trig, qs, lam;
-  int kf, Rc, P0, P1, pv0, pv1, St;
+  int kf, Rc, Rv, P0, P1, pv0, pv1, St;
   int p, ob, inc, red, rvars, rdX;
   int fixm;     // per-stage bit mask of fixed controls (ints)
   int total;    // LDS doubles per scenario
@@ -132,7 +132,7 @@ constexpr Lay make_layout(int N, int m, bool lr, bool refine) {
   L.wstotal = g;
   L.X = o; o += al2(nX); L.Xt = o; o += al2(nX); L.dX = o; o += al2(nX);
   L.trig = o; o += al2(8 * NS); L.qs = o; o += al2(10 * NS); L.lam = o; o += al2(8 * NS);
-  L.kf = o; o += al2(6 * N); L.Rc = o; o += 22;
+  L.kf = o; o += al2(6 * N); L.Rc = o; o += 22; L.Rv = o; o += 8;
   // the Riccati sweep's P / p double buffers: inside `inc` (rollout / adjoint scratch,
   // never live during the sweep) for the LDS-row classes, separate otherwise
   const bool pin = lr && 8 * NS >= 144;
@@ -369,7 +369,7 @@ struct Solver {
   GLB double* gl, *Hl, *Qs;
   LDS double* trig, *qs, *lam;
   GLB double* K, *Rk;
-  LDS double* kf, *Rc, *Pa, *Pb, *pva, *pvb, *St;
+  LDS double* kf, *Rc, *Rv, *Pa, *Pb, *pva, *pvb, *St;
   LDS double* pp, *obx, *oby, *inc, *stamps;
   GLB double* filt;
   LDS int* fixm;  // fixed decision variables (lbx == ubx, make_parameter): bit c of stage k
@@ -386,6 +386,9 @@ struct Solver {
     constexpr Lay L = CAP::L;
     P = (const CST Params*)prm; sm = (LDS double*)smem; this->lane_ = lane_; b = b_;
     N = prm->N; m = prm->m; nobs = prm->nobs; nw = prm->nw; ng = prm->ng; T = prm->T;
+    // the step lives in a VGPR pair: every stage sweep multiplies by it, and as a uniform
+    // SGPR pair it is one of the values spilled to VGPR lanes and restored at each use
+    asm volatile("" : "+v"(T));
     nb = prm->nb; nuE = prm->nuE; nwE = prm->nwE;
     wsbase = wsp;
     GLB double* gw = (GLB double*)(wsp + (long long)b_ * L.wstotal);
@@ -412,7 +415,7 @@ struct Solver {
     wzpR = gw + L.wzpR; wznR = gw + L.wznR; wdpR = gw + L.wdpR; wdnR = gw + L.wdnR; wdyR = gw + L.wdyR;
     gl = gw + L.gl; Hl = gw + L.Hl; trig = sm + L.trig; Qs = gw + L.Qs; qs = sm + L.qs;
     lam = sm + L.lam;
-    K = gw + L.K; kf = sm + L.kf; Rk = gw + L.Rk; Rc = sm + L.Rc;
+    K = gw + L.K; kf = sm + L.kf; Rk = gw + L.Rk; Rc = sm + L.Rc; Rv = sm + L.Rv;
     Pa = sm + L.P0; Pb = sm + L.P1; pva = sm + L.pv0; pvb = sm + L.pv1;
     St = sm + L.St;
     pp = sm + L.p; obx = sm + L.ob; oby = obx + NMPC_MAX_OBS; inc = sm + L.inc;
@@ -629,6 +632,12 @@ struct Solver {
 
   // E entries of A_k = I + E_k and first column b0 of B_k (oracle dyn_jac)
   __device__ __forceinline__ void stage_AB(int k, double& E03, double& E04, double& E13,
+                                           double& E14, double& E23, double& b00, double& b10,
+                                           double& b20) const {
+    stage_AB(k, T, E03, E04, E13, E14, E23, b00, b10, b20);
+  }
+  // ... with the step T passed in (a VGPR copy inside the sweeps)
+  __device__ __forceinline__ void stage_AB(int k, double T, double& E03, double& E04, double& E13,
                                            double& E14, double& E23, double& b00, double& b10,
                                            double& b20) const {
     const LDS double* tg = trig + k * 8;
@@ -935,49 +944,63 @@ struct Solver {
     LDS R* pn = (LDS R*)pvb;
     LDS R* Stc = (LDS R*)St;
     LDS R* Rcc = (LDS R*)Rc;
-    const R Tr = (R)T, dlt = (R)delta;
+    LDS R* rvs = (LDS R*)Rv;  // r_k of the current stage (lanes 0..5 publish, every lane reads)
+    // wave-uniform scalars of the loop held in VGPRs: as SGPR pairs they are spilled to
+    // VGPR lanes and restored (v_readlane pair + s_nop) at every use inside the sweep
+    double Tv = T;
+    R dlt = (R)delta;
+    asm volatile("" : "+v"(Tv), "+v"(dlt));
+    const R Tr = (R)Tv;
     Pc[ln] = (R)Qs[N * 36 + ij];
     if (ln < 8) pc[ln] = (R)qs[N * 10 + ln];
-    // lanes 48..63 -> R~ entries t = 0..15, lanes 0..4 -> t = 16..20 (packed lower)
-    const int tR = ln >= 48 ? ln - 48 : (ln < 5 ? 16 + ln : -1);
+    // lanes 48..63 -> R~ entries t = 0..15, lanes 0..4 -> t = 16..20 (packed lower); the
+    // other lanes duplicate entry 0 (same formula, same value), so every lane stores R~
+    // without a branch
+    const int tR0 = ln >= 48 ? ln - 48 : (ln < 5 ? 16 + ln : -1);
+    const int tR = tR0 >= 0 ? tR0 : 0;
     int rR = 0;
-    while (tR >= 0 && (rR + 1) * (rR + 2) / 2 <= tR) ++rR;
-    const int cR = tR >= 0 ? tR - rR * (rR + 1) / 2 : 0;
+    while ((rR + 1) * (rR + 2) / 2 <= tR) ++rR;
+    const int cR = tR - rR * (rR + 1) / 2;
     const int rowS = (i >= 1 && i < 6) ? 2 + i : 3;
     // stage operands in global memory (Q_k entry, diag R_k entry, r_k) do not depend on
     // the recursion: fetch stage k-1's while stage k is formed, so the sweep never
-    // waits on a global load.  Lanes 0..5 hold r_k (broadcast by readlane).
-    const bool diagR = tR >= 0 && rR == cR;
+    // waits on a global load.  Lanes 0..5 hold r_k and publish it through LDS.  The
+    // fetches and the R~ stores are unconditional (clamped / duplicated addresses: the
+    // lanes that carry no R~ entry recompute entry 0).  The K stores stay with lanes
+    // 0..7: letting the lanes with the same column store duplicates changed the results
+    // at the rounding level (measured against the previous kernel).
+    const bool diagR = rR == cR;
     const int lr = ln < 6 ? ln : 5;
     double qvn = Qs[(N - 1) * 36 + ij];
-    double rdn = (diagR && Rd) ? Rd[(N - 1) * 6 + rR] : 1.0;
+    double rdn = Rd[(N - 1) * 6 + rR];
     double rvn = rv[(N - 1) * 6 + lr];
     // P_k is symmetric: lane (i,j) with i <= j forms entry (i,j) and stores it to both
     // halves; lane 8 = (1,0) is then free to carry r~ through the triangular solves
     const bool upper = i <= j;
     const int ji = j * 8 + i;
+    // Stage-invariant lane roles as 0/1 multipliers (exact: every product with a 0 is an
+    // exact zero added to the one non-zero term), so the stage body has no divergent code:
+    //   A = I + E: column j of E is E03/E13/E23 (j = 3) or E04/E14 (j = 4)
+    const R mj3 = (j == 3) ? (R)1 : (R)0, mj4 = (j == 4) ? (R)1 : (R)0;
+    const R mi3 = (i == 3) ? (R)1 : (R)0, mi4 = (i == 4) ? (R)1 : (R)0;
+    //   S~ row 0 adds s03 (j = 3) / s04 (j = 4)
+    const R ms3 = (i == 0 && j == 3) ? (R)1 : (R)0, ms4 = (i == 0 && j == 4) ? (R)1 : (R)0;
+    const bool absent = diagR && rR >= nuE;  // absent control (model embedding): unit pivot
     sync();
     bool ok = true;
-    for (int k = N - 1; k >= 0; --k) {
-      const R qv = (R)qvn, rdk = (R)rdn, rvk = (R)rvn;
-      if (k > 0) {
-        qvn = Qs[(k - 1) * 36 + ij];
-        if (diagR && Rd) rdn = Rd[(k - 1) * 6 + rR];
-        rvn = rv[(k - 1) * 6 + lr];
-      }
+    // one stage of the backward sweep (false: a pivot is not positive)
+    auto stage = [&](int k, double qvd, double rdd, double rvd) -> bool {
+      const R qv = (R)qvd, rdk = (R)rdd, rvk = (R)rvd;
       double E03d, E04d, E13d, E14d, E23d, b00d, b10d, b20d;
-      stage_AB(k, E03d, E04d, E13d, E14d, E23d, b00d, b10d, b20d);
+      stage_AB(k, Tv, E03d, E04d, E13d, E14d, E23d, b00d, b10d, b20d);
       const R E03 = (R)E03d, E04 = (R)E04d, E13 = (R)E13d, E14 = (R)E14d, E23 = (R)E23d;
       const R b00 = (R)b00d, b10 = (R)b10d, b20 = (R)b20d;
       const R zr = (R)0;
-      // fixed controls (make_parameter) leave the stage problem: unit pivot, no coupling
-      const int fm = nfix > 0 ? fixm[k] : 0;
-      const R aj0 = (j == 3) ? E03 : (j == 4 ? E04 : zr);
-      const R aj1 = (j == 3) ? E13 : (j == 4 ? E14 : zr);
-      const R aj2 = (j == 3) ? E23 : zr;
-      const R ai0 = (i == 3) ? E03 : (i == 4 ? E04 : zr);
-      const R ai1 = (i == 3) ? E13 : (i == 4 ? E14 : zr);
-      const R ai2 = (i == 3) ? E23 : zr;
+      // fixed controls (make_parameter) leave the stage problem: unit pivot, no coupling;
+      // the mask is wave-uniform, so its handling is a scalar branch skipped when 0
+      const int fm = __builtin_amdgcn_readfirstlane(nfix > 0 ? fixm[k] : 0);
+      const R aj0 = mj3 * E03 + mj4 * E04, aj1 = mj3 * E13 + mj4 * E14, aj2 = mj3 * E23;
+      const R ai0 = mi3 * E03 + mi4 * E04, ai1 = mi3 * E13 + mi4 * E14, ai2 = mi3 * E23;
       R APA;
       // ---- (1)
       { STAMP0();
@@ -992,26 +1015,28 @@ struct Solver {
         const R Prj = Pc[rowS * 8 + j], Pr0 = Pc[rowS * 8], Pr1 = Pc[rowS * 8 + 1], Pr2 = Pc[rowS * 8 + 2];
         const R PArj = Prj + ((Pr0 * aj0 + Pr1 * aj1) + Pr2 * aj2);
         R stv = (i == 0) ? ((b00 * PA0j + b10 * PA1j) + b20 * PA2j) : Tr * PArj;
-        stv += (i == 0 && j == 3) ? (R)qs[k * 10 + 8] : ((i == 0 && j == 4) ? (R)qs[k * 10 + 9] : zr);
-        if ((fm >> i) & 1) stv = zr;
-        if (ln < 48) Stc[ln] = stv;
-        if (tR >= 0) {
-          R v;
-          if (rR == 0) {  // b0^T P[0:3,0:3] b0
-            v = b00 * ((P00 * b00 + P01 * b10) + P02 * b20) + b10 * ((P01 * b00 + P11 * b10) + P12 * b20) +
-                b20 * ((P02 * b00 + P12 * b10) + P22 * b20);
-          } else if (cR == 0) {
-            const LDS R* Pr = Pc + (2 + rR) * 8;
-            v = Tr * ((Pr[0] * b00 + Pr[1] * b10) + Pr[2] * b20);
-          } else {
-            v = Tr * (Tr * Pc[(2 + rR) * 8 + 2 + cR]);
-          }
-          // an absent control (model embedding) keeps a unit pivot: zero step, no inertia effect
-          if (rR == cR) v = (rR >= nuE) ? (R)1 : v + (rdk + dlt);
-          if (((fm >> rR) | (fm >> cR)) & 1) v = (rR == cR) ? (R)1 : zr;
-          Rcc[tR] = v;
-          Rk[k * 21 + tR] = (double)v;
+        stv += ms3 * (R)qs[k * 10 + 8] + ms4 * (R)qs[k * 10 + 9];
+        // R~ entry (rR, cR) of B^T P B, B = [b0 | T e_3..7] (lanes that carry no entry
+        // compute entry 0 again: same value, so their store below needs no branch)
+        R v;
+        if (rR == 0) {  // b0^T P[0:3,0:3] b0
+          v = b00 * ((P00 * b00 + P01 * b10) + P02 * b20) + b10 * ((P01 * b00 + P11 * b10) + P12 * b20) +
+              b20 * ((P02 * b00 + P12 * b10) + P22 * b20);
+        } else if (cR == 0) {
+          const LDS R* Pr = Pc + (2 + rR) * 8;
+          v = Tr * ((Pr[0] * b00 + Pr[1] * b10) + Pr[2] * b20);
+        } else {
+          v = Tr * (Tr * Pc[(2 + rR) * 8 + 2 + cR]);
         }
+        if (diagR) v = absent ? (R)1 : v + (rdk + dlt);
+        if (fm != 0) {
+          if ((fm >> i) & 1) stv = zr;
+          if (((fm >> rR) | (fm >> cR)) & 1) v = (rR == cR) ? (R)1 : zr;
+        }
+        if (ln < 48) Stc[ln] = stv;
+        if (tR0 >= 0) Rcc[tR] = v;
+        Rk[k * 21 + tR] = (double)v;
+        if (ln < 6) rvs[ln] = rvk;
         sync();
         STAMP1(PH_RA); }
       // ---- (2)
@@ -1037,17 +1062,20 @@ struct Solver {
             Lm[r * (r + 1) / 2 + c] = v * ig;
           }
         }
-        rt[0] = readlane_d(rvk, 0) + ((b00 * pc[0] + b10 * pc[1]) + b20 * pc[2]);
+        rt[0] = rvs[0] + ((b00 * pc[0] + b10 * pc[1]) + b20 * pc[2]);
 #pragma unroll
-        for (int r = 1; r < 6; ++r) rt[r] = readlane_d(rvk, r) + Tr * pc[2 + r];
+        for (int r = 1; r < 6; ++r) rt[r] = rvs[r] + Tr * pc[2 + r];
+        if (fm != 0) {
 #pragma unroll
-        for (int r = 0; r < 6; ++r)
-          if ((fm >> r) & 1) rt[r] = zr;
+          for (int r = 0; r < 6; ++r)
+            if ((fm >> r) & 1) rt[r] = zr;
+        }
         R ya[6], yb[6];
 #pragma unroll
         for (int r = 0; r < 6; ++r) {
           R a = Stc[r * 8 + i];
-          R bb = (ln == 8) ? rt[r] : Stc[r * 8 + j];
+          R bb = Stc[r * 8 + j];
+          if (ln == 8) bb = rt[r];
 #pragma unroll
           for (int t = 0; t < r; ++t) {
             a -= Lm[r * (r + 1) / 2 + t] * ya[t];
@@ -1064,35 +1092,53 @@ struct Solver {
           Pn[ln] = pv;
           Pn[ji] = pv;
         }
-        if (ln < 9) {
+        // back substitution: lanes 0..7 column ln of K, lane 8 k = -R~^-1 r~ (every lane
+        // computes it: branch-free, so it overlaps with the next stage's LDS reads)
 #pragma unroll
-          for (int r = 5; r >= 0; --r) {
-            R a = yb[r];
+        for (int r = 5; r >= 0; --r) {
+          R a = yb[r];
 #pragma unroll
-            for (int t = r + 1; t < 6; ++t) a -= Lm[t * (t + 1) / 2 + r] * yb[t];
-            yb[r] = a * idg[r];
-          }
-          if (ln < 8) {
+          for (int t = r + 1; t < 6; ++t) a -= Lm[t * (t + 1) / 2 + r] * yb[t];
+          yb[r] = a * idg[r];
+        }
+        R atp = pc[j];
+        atp = atp + mj3 * ((E03 * pc[0] + E13 * pc[1]) + E23 * pc[2]) + mj4 * (E04 * pc[0] + E14 * pc[1]);
+        R kr = zr;
 #pragma unroll
-            for (int r = 0; r < 6; ++r) K[k * 48 + r * 8 + ln] = (double)(-yb[r]);
-            R atp = pc[ln];
-            if (ln == 3) atp = atp + ((E03 * pc[0] + E13 * pc[1]) + E23 * pc[2]);
-            else if (ln == 4) atp = atp + (E04 * pc[0] + E14 * pc[1]);
-            R kr = zr;
+        for (int r = 0; r < 6; ++r) kr += (-yb[r]) * rt[r];
+        const R pnv = ((R)qs[k * 10 + j] + atp) + kr;
+        if (ln < 8) {
 #pragma unroll
-            for (int r = 0; r < 6; ++r) kr += (-yb[r]) * rt[r];
-            pn[ln] = ((R)qs[k * 10 + ln] + atp) + kr;
-          } else {
+          for (int r = 0; r < 6; ++r) K[k * 48 + r * 8 + ln] = (double)(-yb[r]);
+        }
+        if (ln < 8) {
+          pn[ln] = pnv;
+        } else if (ln == 8) {
 #pragma unroll
-            for (int r = 0; r < 6; ++r) kf[k * 6 + r] = (double)(-yb[r]);
-          }
+          for (int r = 0; r < 6; ++r) kf[k * 6 + r] = (double)(-yb[r]);
         }
         sync();
         STAMP1(PH_RD); }
       ok = !wany(!ok);  // every lane computed the same pivots; make it explicit
-      if (!ok) break;
+      if (!ok) return false;
       LDS R* t1 = Pc; Pc = Pn; Pn = t1;
       LDS R* t2 = pc; pc = pn; pn = t2;
+      return true;
+    };
+    // two stages per trip, their prefetched operands in alternating registers: no
+    // loop-carried register copies (which made the loop latch wait for every store)
+    double qB, rB, vB;
+    for (int k = N - 1; k >= 0; k -= 2) {
+      {
+        const int kp = k > 0 ? k - 1 : 0;
+        qB = Qs[kp * 36 + ij]; rB = Rd[kp * 6 + rR]; vB = rv[kp * 6 + lr];
+      }
+      if (!stage(k, qvn, rdn, rvn) || k == 0) break;
+      {
+        const int kp = k > 1 ? k - 2 : 0;
+        qvn = Qs[kp * 36 + ij]; rdn = Rd[kp * 6 + rR]; rvn = rv[kp * 6 + lr];
+      }
+      if (!stage(k - 1, qB, rB, vB)) break;
     }
     return ok;
   }
@@ -1269,26 +1315,14 @@ struct Solver {
     const int r = ln < 6 ? ln : 5;
     // K_k rows come from global memory and do not depend on dx: fetch stage k+1's
     // row while stage k is being formed
-    double Kn[8];
-#pragma unroll
-    for (int c = 0; c < 8; ++c) Kn[c] = K[r * 8 + c];
-    double kn = kf[r];
-    for (int k = 0; k < N; ++k) {
-      double Kr[8];
-#pragma unroll
-      for (int c = 0; c < 8; ++c) Kr[c] = Kn[c];
-      const double kk = kn;
-      if (k + 1 < N) {
-#pragma unroll
-        for (int c = 0; c < 8; ++c) Kn[c] = K[(k + 1) * 48 + r * 8 + c];
-        kn = kf[(k + 1) * 6 + r];
-      }
+    // one stage: du_k = K_k dx_k + k_k (lanes 0..5), dx_{k+1} = A_k dx_k + B_k du_k
+    auto stage = [&](int k, const double (&Kr)[8], double kk) {
       double E03, E04, E13, E14, E23, b00, b10, b20;
       stage_AB(k, E03, E04, E13, E14, E23, b00, b10, b20);
       double a = kk;
 #pragma unroll
       for (int c = 0; c < 8; ++c) a += Kr[c] * dx[c];
-      if (ln < 6) dUo[k * 6 + ln] = a;
+      dUo[k * 6 + r] = a;  // lanes >= 5 all hold row 5: same value, same address
       double du_[6];
 #pragma unroll
       for (int q = 0; q < 6; ++q) du_[q] = readlane_d(a, q);
@@ -1304,6 +1338,31 @@ struct Solver {
       }
 #pragma unroll
       for (int c = 0; c < 8; ++c) dx[c] = xn[c];
+    };
+    // K_k rows come from global memory and do not depend on dx: stage k+1's row is
+    // fetched while stage k is formed, into the other of two register sets (two stages
+    // per trip, so no register copies between stages)
+    double KA[8], KB[8], kA, kB;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) KA[c] = K[r * 8 + c];
+    kA = kf[r];
+    // (fetches clamped to the last stage rather than guarded: no branch, see riccati_)
+    for (int k = 0; k < N; k += 2) {
+      {
+        const int kb = k + 1 < N ? k + 1 : N - 1;
+#pragma unroll
+        for (int c = 0; c < 8; ++c) KB[c] = K[kb * 48 + r * 8 + c];
+        kB = kf[kb * 6 + r];
+      }
+      stage(k, KA, kA);
+      if (k + 1 >= N) break;
+      {
+        const int ka = k + 2 < N ? k + 2 : N - 1;
+#pragma unroll
+        for (int c = 0; c < 8; ++c) KA[c] = K[ka * 48 + r * 8 + c];
+        kA = kf[ka * 6 + r];
+      }
+      stage(k + 1, KB, kB);
     }
     sync();
     STAMP1(PH_FWD);
@@ -3563,6 +3622,8 @@ using CapC = Cap<63, 21>;   // any supported shape
 using CapD = Cap<50, 15>;
 // fp32 Riccati factorisation (nmpc_options.linear_solver_fp32; BASELINE config 5's fp32 leg)
 using CapA32 = Cap<20, 15, true, float>;
+// the LDS-row classes run four scenarios per CU (160 KB of LDS): one wave per SIMD
+static_assert(CapA::L.total * 8 <= 40960 && CapA32::L.total * 8 <= 40960, "LDS-row class exceeds a quarter CU");
 using CapC32 = Cap<63, 21, false, float>;
 
 #ifdef NMPC_TU_CLASS
