@@ -616,8 +616,13 @@ class IpoptDense:
         lbx, ubx = np.asarray(lbx, float).ravel(), np.asarray(ubx, float).ravel()
         lbg, ubg = np.asarray(lbg, float).ravel(), np.asarray(ubg, float).ravel()
         w0 = np.asarray(x0, float).ravel()
-        if np.any((np.abs(lbg) < INF) & (lbg == ubg)):
-            raise ValueError("equality rows (lbg == ubg) are not supported")
+        # equality rows (lbg == ubg): IPOPT's TNLPAdapter makes them c(x) = g(x) - g_l = 0,
+        # with a multiplier and no slack, no bound multipliers and no bound relaxation.  Here
+        # they keep a row slot whose "slack" is pinned at the (scaled) target, so d - s = c
+        # enters theta, the residuals and the filter unchanged; the Newton step treats them
+        # through the Schur complement of the augmented system (solve_dir).
+        eq = (np.abs(lbg) < INF) & (lbg == ubg)
+        neq = int(eq.sum())
         # fixed variables (lbx == ubx): IPOPT's default fixed_variable_treatment =
         # make_parameter (TNLPAdapter) removes them from the NLP -- held at the bound,
         # no bound multipliers, no step, excluded from the scaling maxima and the
@@ -633,7 +638,7 @@ class IpoptDense:
             return M_ if nf == n else M_[np.ix_(F, F)]
         w0 = np.where(fixed, lbx, w0)
         xlm, xum = (lbx > -INF) & fr, (ubx < INF) & fr
-        slm, sum_ = lbg > -INF, ubg < INF
+        slm, sum_ = (lbg > -INF) & ~eq, (ubg < INF) & ~eq
         xl, xu = self._relax(lbx, -1.0), self._relax(ubx, +1.0)
         gl_, gu_ = self._relax(lbg, -1.0), self._relax(ubg, +1.0)
         damp_xl = (xlm & ~xum).astype(float)
@@ -665,6 +670,7 @@ class IpoptDense:
         x = self._push(w0, xl, xu, xlm, xum, o["bound_push"], o["bound_frac"])
         ev = self._evaluate(x)
         s = self._push(dc * ev.g, dl, du, slm, sum_, o["slack_bound_push"], o["slack_bound_frac"])
+        s = np.where(eq, dc * lbg, s)  # equality rows: pinned at the scaled target
         zl = np.where(xlm, o["bound_mult_init_val"], 0.0)
         zu = np.where(xum, o["bound_mult_init_val"], 0.0)
         vl = np.where(slm, o["bound_mult_init_val"], 0.0)
@@ -674,8 +680,7 @@ class IpoptDense:
             J = dc[:, None] * ev.J[:, F]
             bx = (df * ev.gradF - zl + zu)[F]
             bs = vu - vl
-            wx = np.linalg.solve(np.eye(nf) + J.T @ J, bx + J.T @ bs)
-            y = bs - J @ wx
+            y = ls_mults(J, bx, bs, eq)
             if np.max(np.abs(y)) > o["constr_mult_init_max"]:
                 y = np.zeros(m)
         mu = o["mu_init"]
@@ -701,7 +706,8 @@ class IpoptDense:
             return val
 
         def grad_lag(gf, J, y_, zl_, zu_, vl_, vu_):
-            return np.where(fr, gf + J.T @ y_ - zl_ + zu_, 0.0), -y_ - vl_ + vu_
+            # the slack components exist for the inequality rows only
+            return np.where(fr, gf + J.T @ y_ - zl_ + zu_, 0.0), np.where(eq, 0.0, -y_ - vl_ + vu_)
 
         def compl(x_, s_, zl_, zu_, vl_, vu_, mu_):
             Sxl, Sxu, Ssl, Ssu = slacks(x_, s_)
@@ -767,7 +773,8 @@ class IpoptDense:
             sd, sc = err_scaling(y_, zl_, zu_, vl_, vu_)
             glx, gls = grad_lag(gf_, J_, y_, zl_, zu_, vl_, vu_)
             dinf = max(amax(glx), amax(gls))
-            cviol = amax(np.concatenate([np.maximum(0.0, dl - d_)[slm], np.maximum(0.0, d_ - du)[sum_]]))
+            cviol = amax(np.concatenate([np.maximum(0.0, dl - d_)[slm], np.maximum(0.0, d_ - du)[sum_],
+                                         np.abs(d_ - s_)[eq]]))
             cmp = amax(compl(x_, s_, zl_, zu_, vl_, vu_, 0.0))
             return max(dinf / sd, cviol, cmp / sc), dinf, cviol, cmp
 
@@ -779,7 +786,7 @@ class IpoptDense:
 
         def pd_error(x_, s_, d_, gf_, J_, y_, zl_, zu_, vl_, vu_, mu_):
             glx, gls = grad_lag(gf_, J_, y_, zl_, zu_, vl_, vu_)
-            dual = (np.sum(np.abs(glx)) + np.sum(np.abs(gls))) / (nf + m)
+            dual = (np.sum(np.abs(glx)) + np.sum(np.abs(gls))) / (nf + m - neq)
             prim = np.sum(np.abs(d_ - s_)) / m if m else 0.0
             nc = nzx + nzs
             cm = np.sum(np.abs(compl(x_, s_, zl_, zu_, vl_, vu_, mu_))) / nc if nc else 0.0
@@ -825,8 +832,7 @@ class IpoptDense:
                 Jfull = np.hstack([JR[:, F], -np.eye(m), np.eye(m)])
                 bx = np.concatenate([(eta(muR) * DR2 * (xR_ - xR) - zlR + zuR)[F], rho - zp, rho - zn])
                 bs = vuR - vlR
-                wx = np.linalg.solve(np.eye(nf + 2 * m) + Jfull.T @ Jfull, bx + Jfull.T @ bs)
-                yR = bs - Jfull @ wx
+                yR = ls_mults(Jfull, bx, bs, eq)
                 if np.max(np.abs(yR)) > o["constr_mult_init_max"]:
                     yR = np.zeros(m)
             nzp = 2 * m  # p, n: lower bounds only
@@ -853,11 +859,12 @@ class IpoptDense:
             def errR(x_, s_, d_, J_, p_, n_, y_, zl_, zu_, vl_, vu_, zp_, zn_, mu_, mu_c):
                 """(overall error, dual inf, constraint violation, complementarity) of the resto NLP."""
                 glx = np.where(fr, eta(mu_) * DR2 * (x_ - xR) + J_.T @ y_ - zl_ + zu_, 0.0)
-                gls = -y_ - vl_ + vu_
+                gls = np.where(eq, 0.0, -y_ - vl_ + vu_)
                 glp, gln = rho - y_ - zp_, rho + y_ - zn_
                 dinf_ = max(amax(glx), amax(gls), amax(glp), amax(gln))
                 dr = d_ - p_ + n_
-                cv = amax(np.concatenate([np.maximum(0.0, dl - dr)[slm], np.maximum(0.0, dr - du)[sum_]]))
+                cv = amax(np.concatenate([np.maximum(0.0, dl - dr)[slm], np.maximum(0.0, dr - du)[sum_],
+                                          np.abs(dr - s_)[eq]]))
                 cm = amax(np.concatenate([compl(x_, s_, zl_, zu_, vl_, vu_, mu_c), p_ * zp_ - mu_c, n_ * zn_ - mu_c]))
                 smax = o["s_max"]
                 nd = m + nzx + nzs + nzp
@@ -922,7 +929,7 @@ class IpoptDense:
                     racc = 0
                 if conv or (o["acceptable_iter"] > 0 and racc >= o["acceptable_iter"]):
                     # converged restoration problem: original infeasibility not reducible
-                    if cviol_unscaled(dR, dc, gl_, gu_, slm, sum_) > o["constr_viol_tol"]:
+                    if cviol_unscaled(dR, dc, gl_, gu_, slm, sum_, eq, lbg) > o["constr_viol_tol"]:
                         return dict(status=INFEASIBLE_PROBLEM_DETECTED, it=it_, x=xx)
                     break
                 if it_ >= o["max_iter"]:
@@ -933,7 +940,7 @@ class IpoptDense:
                     e_, _, _, _, sd_, sc_, pinf_ = errR(xx, ss, dR, JR, pp, nn, yR, zlR, zuR, vlR, vuR, zp, zn,
                                                         mu_, mu_)
                     glx = np.where(fr, eta(mu_) * DR2 * (xx - xR) + JR.T @ yR - zlR + zuR, 0.0)
-                    gls = -yR - vlR + vuR
+                    gls = np.where(eq, 0.0, -yR - vlR + vuR)
                     dinf_ = max(amax(glx), amax(gls), amax(rho - yR - zp), amax(rho + yR - zn))
                     cm_ = amax(np.concatenate([compl(xx, ss, zlR, zuR, vlR, vuR, mu_), pp * zp - mu_,
                                                nn * zn - mu_]))
@@ -975,6 +982,7 @@ class IpoptDense:
                     D_ = SigS + delta_
                     Spd, Snd = Sp + delta_, Sn + delta_
                     Dt = D_ / (1.0 + D_ * (1.0 / Spd + 1.0 / Snd))
+                    Dt = np.where(eq, 1.0 / (1.0 / Spd + 1.0 / Snd), Dt)  # equality rows: D = inf
                     # row weight D~ = (1/D + 1/Sp + 1/Sn)^-1 (p, n eliminated); written
                     # without 1/D so rows with no bound (D = 0) stay finite
                     M = Wr + np.diag(SigX + delta_) + JR.T @ (Dt[:, None] * JR)
@@ -1000,6 +1008,8 @@ class IpoptDense:
                 Spd, Snd = Sp + delta_, Sn + delta_
                 den = 1.0 / (1.0 + D_ * (1.0 / Spd + 1.0 / Snd))
                 Dt = D_ * den
+                den = np.where(eq, 0.0, den)  # equality rows (no slack): the D -> inf limit
+                Dt = np.where(eq, 1.0 / (1.0 / Spd + 1.0 / Snd), Dt)
 
                 def rdir(c_):
                     # dy = D~ (J dx + c + rs/D + rp/Sp - rn/Sn), with D~ rs/D = rs * den
@@ -1011,7 +1021,7 @@ class IpoptDense:
                     dy_ = Dt * jd + Dr
                     dp_ = (dy_ - rp) / Spd
                     dn_ = (-dy_ - rn) / Snd
-                    ds_ = jd + c_ - dp_ + dn_  # linearised d(x) - s - p + n = 0
+                    ds_ = np.where(eq, 0.0, jd + c_ - dp_ + dn_)  # linearised d(x) - s - p + n = 0
                     dzl_ = np.where(xlm, muR / Sxl - zlR - zlR / Sxl * dx_, 0.0)
                     dzu_ = np.where(xum, muR / Sxu - zuR + zuR / Sxu * dx_, 0.0)
                     dvl_ = np.where(slm, muR / Ssl - vlR - vlR / Ssl * ds_, 0.0)
@@ -1200,7 +1210,7 @@ class IpoptDense:
             if not np.isfinite(err):
                 status = INVALID_NUMBER_DETECTED
                 break
-            u_dinf, u_cviol, u_cmp = dinf / df, cviol_unscaled(d, dc, gl_, gu_, slm, sum_), cmp / df
+            u_dinf, u_cviol, u_cmp = dinf / df, cviol_unscaled(d, dc, gl_, gu_, slm, sum_, eq, lbg), cmp / df
             if (err <= o["tol"] and u_dinf <= o["dual_inf_tol"] and u_cviol <= o["constr_viol_tol"]
                     and u_cmp <= o["compl_inf_tol"]):
                 status = SOLVE_SUCCEEDED
@@ -1266,10 +1276,15 @@ class IpoptDense:
             delta = 0.0
             fact = None
             while True:
-                D = SigS + delta
+                D = np.where(eq, 0.0, SigS + delta)
                 M = W + np.diag(SigX + delta) + J.T @ (D[:, None] * J)
                 try:
-                    fact = np.linalg.cholesky(sq(M))
+                    if neq:  # the augmented system's inertia (PDPerturbationHandler)
+                        fact = eq_kkt(sq(M), J[eq][:, F], mu)
+                        if fact is None:
+                            raise np.linalg.LinAlgError("wrong inertia of the augmented system")
+                    else:
+                        fact = np.linalg.cholesky(sq(M))
                     break
                 except np.linalg.LinAlgError:
                     if delta == 0.0:
@@ -1287,15 +1302,23 @@ class IpoptDense:
             if fact is None:
                 status = ERROR_IN_STEP_COMPUTATION
                 break
-            D = SigS + delta
+            D = np.where(eq, 0.0, SigS + delta)
 
             def solve_dir(rd_):
-                rhs = -(gphi + J.T @ (y + D * rd_ + rs))
-                t = np.linalg.solve(fact, rhs[F])
+                # equality rows contribute J_c^T y_c to the gradient, no slack elimination
+                rhs = -(gphi + J.T @ np.where(eq, y, y + D * rd_ + rs))
                 dx_ = np.zeros(n)
-                dx_[F] = np.linalg.solve(fact.T, t)
-                ds_ = J @ dx_ + rd_
+                dyc = None
+                if neq:  # [M J_c^T; J_c -delta_c I] [dx; dy_c] = [rhs; -c]
+                    sol = np.linalg.solve(fact, np.concatenate([rhs[F], -rd_[eq]]))
+                    dx_[F], dyc = sol[:nf], sol[nf:]
+                else:
+                    t = np.linalg.solve(fact, rhs[F])
+                    dx_[F] = np.linalg.solve(fact.T, t)
+                ds_ = np.where(eq, 0.0, J @ dx_ + rd_)
                 dy_ = D * ds_ + rs
+                if neq:
+                    dy_[eq] = dyc
                 dzl_ = np.where(xlm, mu / Sxl - zl - zl / Sxl * dx_, 0.0)
                 dzu_ = np.where(xum, mu / Sxu - zu + zu / Sxu * dx_, 0.0)
                 dvl_ = np.where(slm, mu / Ssl - vl - vl / Ssl * ds_, 0.0)
@@ -1566,11 +1589,64 @@ class IpoptDense:
                     X=X, status=status, iter=it, trace=tr, df=df, dc=dc, mu=mu)
 
 
-def cviol_unscaled(d, dc, gl_, gu_, slm, sum_):
-    """Unscaled constraint violation (max norm) w.r.t. the relaxed bounds."""
+def cviol_unscaled(d, dc, gl_, gu_, slm, sum_, eq=None, gE=None):
+    """Unscaled constraint violation (max norm) w.r.t. the relaxed bounds; equality rows
+    (eq) by |g - g_E|."""
     g = d / dc
-    v = np.concatenate([np.maximum(0.0, gl_ - g)[slm], np.maximum(0.0, g - gu_)[sum_]])
+    parts = [np.maximum(0.0, gl_ - g)[slm], np.maximum(0.0, g - gu_)[sum_]]
+    if eq is not None:
+        parts.append(np.abs(g - gE)[eq])
+    v = np.concatenate(parts)
     return float(np.max(v)) if v.size else 0.0
+
+
+def ls_mults(J, bx, bs, eq):
+    """IPOPT's least-squares constraint multipliers (LeastSquareMults): min |wx - bx|^2 +
+    |ws - bs|^2 subject to J_d wx - ws = 0 (inequality rows, slack ws) and J_c wx = 0
+    (equality rows); y = bs - J_d wx on the inequality rows (the sign convention of the
+    plain formula (I + J^T J) wx = bx + J^T bs, y = bs - J wx, used when there are none)."""
+    if not np.any(eq):
+        wx = np.linalg.solve(np.eye(J.shape[1]) + J.T @ J, bx + J.T @ bs)
+        return bs - J @ wx
+    Jd, Jc = J[~eq], J[eq]
+    nx, nc = J.shape[1], int(eq.sum())
+    K = np.zeros((nx + nc, nx + nc))
+    K[:nx, :nx] = np.eye(nx) + Jd.T @ Jd
+    K[:nx, nx:] = -Jc.T
+    K[nx:, :nx] = Jc
+    sol = np.linalg.solve(K, np.concatenate([bx + Jd.T @ bs[~eq], np.zeros(nc)]))
+    y = np.zeros(J.shape[0])
+    y[~eq] = bs[~eq] - Jd @ sol[:nx]
+    y[eq] = sol[nx:]
+    return y
+
+
+def eq_kkt(M, Jc, mu, reg_value=1e-8, reg_exponent=0.25):
+    """The augmented Newton matrix K = [M J_c^T; J_c -delta_c I] of a problem with
+    equality rows (M: the condensed Hessian block, inequality rows eliminated) when its
+    inertia is IPOPT's (n positive, m_c negative eigenvalues), else None.  By Haynsworth,
+    inertia(K) = inertia(M) + inertia(-(S + delta_c I)), S = J_c M^-1 J_c^T, so with k
+    negative eigenvalues of M the test is: S + delta_c I has exactly k negative ones (the
+    kernel reads k from the signs of its Riccati pivots).  A singular S (rank-deficient
+    J_c; eigenvalues below 1e-14 of its largest) gets IPOPT's delta_c =
+    jacobian_regularization_value * mu^jacobian_regularization_exponent; a wrong inertia, a
+    singular M or a still singular S returns None (the caller raises delta_w)."""
+    evM = np.linalg.eigvalsh(M)
+    if np.any(evM == 0.0):
+        return None
+    k = int(np.sum(evM < 0.0))
+    S = Jc @ np.linalg.solve(M, Jc.T)
+    mc = S.shape[0]
+    for dcv in (0.0, reg_value * mu ** reg_exponent):
+        ev = np.linalg.eigvalsh(S + dcv * np.eye(mc))
+        scale = float(np.max(np.abs(ev)))
+        if scale == 0.0 or np.any(np.abs(ev) <= 1e-14 * scale):
+            continue
+        if int(np.sum(ev < 0.0)) != k:
+            return None
+        return np.block([[M, Jc.T], [Jc, -dcv * np.eye(mc)]])
+    return None
+    return None
 
 
 # --- closed loop (immediate caller, Python/NMPC_TT.py:13-30, :346-402) --------

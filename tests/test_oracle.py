@@ -189,3 +189,77 @@ def test_no_gimbal_model_functions_and_bounds():
         assert abs(ev.gradF[j] - fd) <= 1e-6 * (1 + abs(fd))
         fdg = (orc.constraints(prob5, w5 + e, p5) - orc.constraints(prob5, w5 - e, p5)) / (2 * h)
         np.testing.assert_allclose(ev.J[:, j], fdg, atol=1e-6)
+
+
+def _pinned_z_problem(b, dz=1.0, k=6):
+    """Race Track 2 layout, N = 8: z at stage k pinned (lbg == ubg) to the free optimum's
+    height + dz, a reachable target (|dz| is within a few steps' climb)."""
+    from nmpc_amd import make_spec, draw_scenarios
+    prob = orc.make_problem("race_track_2", N=8, T=0.2)
+    p = draw_scenarios(make_spec("race_track_2", N=8, T=0.2), 4, seed=11)[b]
+    lbx, ubx, lbg, ubg = orc.bounds(prob)
+    r0 = orc.IpoptDense(prob, orc.REFERENCE_OPTS).solve(np.zeros(prob.nw), lbx, ubx, lbg, ubg, p)
+    X0 = orc.rollout(prob, np.reshape(r0["x"], (6, prob.N), order="F"), p[:8])
+    row = k * prob.m
+    lbg, ubg = lbg.copy(), ubg.copy()
+    lbg[row] = ubg[row] = X0[2, k] + dz
+    return prob, p, lbx, ubx, lbg, ubg, row
+
+
+@pytest.mark.parametrize("b", [0, 1, 2])
+def test_equality_row_solved_as_ipopt_does(b):
+    """lbg == ubg: c(x) = 0 through the augmented system (Schur complement, Haynsworth
+    inertia test).  Checked against SciPy SLSQP's objective on the same NLP and by the KKT
+    certificate of the returned point."""
+    from scipy.optimize import minimize
+    prob, p, lbx, ubx, lbg, ubg, row = _pinned_z_problem(b)
+    r = orc.IpoptDense(prob, orc.REFERENCE_OPTS).solve(np.zeros(prob.nw), lbx, ubx, lbg, ubg, p)
+    assert r["status"] == orc.SOLVE_SUCCEEDED
+    g = orc.constraints(prob, r["x"], p)
+    assert abs(g[row] - lbg[row]) <= 1e-6
+    ineq = np.isfinite(lbg) & (lbg != ubg), np.isfinite(ubg) & (lbg != ubg)
+    cons = [{"type": "eq", "fun": lambda w: orc.constraints(prob, w, p)[row] - lbg[row]},
+            {"type": "ineq", "fun": lambda w: np.concatenate([(orc.constraints(prob, w, p) - lbg)[ineq[0]],
+                                                             (ubg - orc.constraints(prob, w, p))[ineq[1]]])}]
+    sl = minimize(lambda w: orc.objective(prob, w, p), r["x"], method="SLSQP", bounds=list(zip(lbx, ubx)),
+                  constraints=cons, options={"maxiter": 500, "ftol": 1e-12})
+    assert sl.success and r["f"] <= sl.fun + 1e-6 * (1 + abs(sl.fun))
+    # stationarity with the returned multipliers (CasADi's sign convention)
+    ev = orc.SSEval(prob, r["x"], p)
+    res = ev.gradF + ev.J.T @ r["lam_g"] + r["lam_x"]
+    assert np.max(np.abs(res)) <= 1e-5 * (1 + np.max(np.abs(ev.gradF)))
+
+
+@pytest.mark.parametrize("N,n_eq", [(16, 8), (20, 40)])
+def test_reference_bounds_at_n_not_15_are_equality_rows(N, n_eq):
+    """Python/NMPC_TT.py:271-291 run at N != 15 leaves the rows past index 128
+    at lbg = ubg = 0 (z = 0, theta = 0, ... and every obstacle row active): equality rows of
+    an infeasible NLP.  IPOPT's path for it -- restoration, then Infeasible_Problem_Detected
+    -- is restated; the kernel test (tests/test_gpu_equality.py) compares with this."""
+    lbx, ubx, lbg, ubg = reference_bounds_literal(N)
+    assert int(np.sum(lbg == ubg)) == n_eq
+    prob = orc.make_problem("nmpc_tt", N=N, T=1.0)
+    p = np.array([90, 150, 80, 0, 0, 0, 0, 0, 100, 150, 0.0])  # Python/NMPC_TT.py:57-58,316-339
+    r = orc.IpoptDense(prob, orc.REFERENCE_OPTS).solve(np.zeros(prob.nw), lbx, ubx, lbg, ubg, p)
+    assert r["status"] == orc.INFEASIBLE_PROBLEM_DETECTED
+
+
+def reference_bounds_literal(N, m_rows=8, n_obs=3, stop=128):
+    """Python/NMPC_TT.py:269-306 verbatim for any N: lbg/ubg sized n_states_u*(N+1), the
+    row slices hard-coded to stop at 128 (F3), lbx/ubx sliced with N."""
+    lbg = np.zeros(m_rows * (N + 1))
+    ubg = np.zeros_like(lbg)
+    lbg[0:stop:m_rows] = 75; ubg[0:stop:m_rows] = 150
+    lbg[1:stop:m_rows] = -0.2618; ubg[1:stop:m_rows] = 0.2618
+    lbg[2:stop:m_rows] = -math.pi / 6; ubg[2:stop:m_rows] = math.pi / 6
+    lbg[3:stop:m_rows] = -math.pi / 6; ubg[3:stop:m_rows] = math.pi / 6
+    lbg[4:stop:m_rows] = -math.pi / 2; ubg[4:stop:m_rows] = math.pi / 2
+    for j in range(5, 5 + n_obs):
+        lbg[j:stop:m_rows] = -np.inf
+        ubg[j:stop:m_rows] = 0
+    lbx = np.zeros(6 * N); ubx = np.zeros(6 * N)
+    for j, (lo, hi) in enumerate([(14, 30), (-math.pi / 30, math.pi / 30), (-math.pi / 21, math.pi / 21),
+                                  (-math.pi / 30, math.pi / 30), (-math.pi / 30, math.pi / 30),
+                                  (-math.pi / 30, math.pi / 30)]):
+        lbx[j:6 * N:6] = lo; ubx[j:6 * N:6] = hi
+    return lbx, ubx, lbg, ubg
