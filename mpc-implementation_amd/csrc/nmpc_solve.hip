@@ -49,6 +49,9 @@ constexpr int WAVE = 64;
 constexpr double BIGB = 1e19;  // IPOPT nlp_{lower,upper}_bound_inf
 constexpr int FCAP = 128;      // filter capacity (>= max_iter of the reference opts)
 constexpr int TRACE_F = NMPC_TRACE_FIELDS;
+// equality rows (lbg == ubg) per problem the augmented-system (Schur complement) step
+// supports; more report Invalid_Problem_Definition (-11)
+#define NMPC_MEQ 16
 
 // ---- status codes (IPOPT ApplicationReturnStatus) ----
 constexpr int ST_SUCCESS = 0, ST_ACCEPTABLE = 1, ST_INFEASIBLE = 2, ST_TINY = 3, ST_MAXITER = -1,
@@ -78,6 +81,7 @@ struct Lay {
   // restoration phase: reference/backup iterate, p/n and their multipliers, steps, filter
   int UR, zl0, zu0, s0, vl0, vu0, pR, nR, zpR, znR, dpR, dnR, dyR, dp2R, dn2R, dy2R, cms, filtR;
   int accU, accZl, accZu, accY;  // last acceptable iterate (BacktrackingLineSearch::StoreAcceptablePoint)
+  int eqi, eqS, eqy, eqy2;        // equality rows: indices, Schur factor, dy_c (row-indexed) of the step / SOC
   // watchdog procedure: the stored iterate and its step (main loop; the restoration phase
   // reuses them, and adds its p, n, their multipliers and steps)
   int wU, wzl, wzu, wdU, ws, wy, wvl, wvu, wds, wpR, wnR, wzpR, wznR, wdpR, wdnR, wdyR;
@@ -95,7 +99,7 @@ constexpr int al8(int n) { return (n + 7) & ~7; }
 // lr: the main iteration's hot row vectors (s, y, vl, vu, d, ds, ds2, dc) live in LDS
 // (capacity classes with a small row count: the row passes then never wait on L2 /
 // Infinity-Cache latency); otherwise in the global workspace
-constexpr Lay make_layout(int N, int m, bool lr, bool refine) {
+constexpr Lay make_layout(int N, int m, bool lr, bool refine, bool eq) {
   Lay L{};
   const int nw = 6 * N, ng = m * (N + 1), nX = 8 * (N + 1), NS = N + 1;
   int g = 0, o = 0;
@@ -129,6 +133,10 @@ constexpr Lay make_layout(int N, int m, bool lr, bool refine) {
   L.ws = g; g += al8(ng); L.wy = g; g += al8(ng); L.wvl = g; g += al8(ng); L.wvu = g; g += al8(ng);
   L.wds = g; g += al8(ng); L.wpR = g; g += al8(ng); L.wnR = g; g += al8(ng); L.wzpR = g; g += al8(ng);
   L.wznR = g; g += al8(ng); L.wdpR = g; g += al8(ng); L.wdnR = g; g += al8(ng); L.wdyR = g; g += al8(ng);
+  if (eq) {  // equality rows (the equality class only)
+    L.eqi = g; g += al8(NMPC_MEQ / 2 + 1); L.eqS = g; g += al8(NMPC_MEQ * NMPC_MEQ + NMPC_MEQ);
+    L.eqy = g; g += al8(ng); L.eqy2 = g; g += al8(ng);
+  }
   L.wstotal = g;
   L.X = o; o += al2(nX); L.Xt = o; o += al2(nX); L.dX = o; o += al2(nX);
   L.trig = o; o += al2(8 * NS); L.qs = o; o += al2(10 * NS); L.lam = o; o += al2(8 * NS);
@@ -167,7 +175,9 @@ constexpr Lay make_layout(int N, int m, bool lr, bool refine) {
 // RT: arithmetic type of the Riccati factorisation and its solves (double: the
 // reference's fp64; float: the fp32 leg of BASELINE config 5's fp32-vs-fp64 sweep --
 // everything else, the iterate, residuals, line search and termination tests, stays fp64)
-template <int NMAX, int MMAX, bool LDSR = false, class RTYPE = double>
+// EQ: equality rows (lbg == ubg) are solved; only the equality class has
+// them compiled in, so the other classes' hot loops carry none of that code
+template <int NMAX, int MMAX, bool LDSR = false, class RTYPE = double, bool EQ = false>
 struct Cap {
   static constexpr int nmax = NMAX, mmax = MMAX;
   static constexpr bool lds_rows = LDSR;
@@ -175,7 +185,9 @@ struct Cap {
   static constexpr int wpe = LDSR ? 1 : NMPC_WAVES_PER_EU;
   using RowT = std::conditional_t<LDSR, LDS double, GLB double>;
   static constexpr bool refine = !std::is_same<RTYPE, double>::value;  // fp64 refinement of fp32 solves
-  static constexpr Lay L = make_layout(NMAX, MMAX, LDSR, refine);
+  static constexpr bool eq = EQ;
+  static_assert(!(EQ && !std::is_same<RTYPE, double>::value), "equality rows need the fp64 factorisation");
+  static constexpr Lay L = make_layout(NMAX, MMAX, LDSR, refine, EQ);
   // row passes: trips of 64 rows processed together (their loads batched), <= 5
   static constexpr int rtrips = (MMAX * (NMAX + 1) + 63) / 64;
   static constexpr int ru = rtrips < 2 ? rtrips : 2;
@@ -188,6 +200,10 @@ struct IO {
   int *status, *iters;
   double* trace;
   double* ws;  // per-scenario global workspace, B x wstotal
+  // launch gate (nullable): 1 when the batch has equality rows.  A class kernel whose
+  // CAP::eq differs from it returns at once, so the host enqueues the problem's class and
+  // the equality class back to back and exactly one of them runs (no host round trip)
+  const int* eqflag;
 };
 
 // Wave-wide all-reduces without LDS: DPP within 16-lane rows (quad_perm xor1,
@@ -361,6 +377,8 @@ struct Solver {
   GLB double* dms;
   GLB double *UR, *zl0, *zu0, *s0, *vl0, *vu0, *pR, *nR, *zpR, *znR, *dpR, *dnR, *dyR, *dp2R, *dn2R, *dy2R, *cms, *filtR;
   GLB double *accU, *accZl, *accZu, *accY;
+  int meq;                       // number of equality rows (0: none, the common case)
+  int nneg;                      // negative Riccati pivots of the last factorization (SG sweeps)
   GLB double *wU, *wzl, *wzu, *wdU, *wsl, *wy, *wvl, *wvu, *wds, *wpR, *wnR, *wzpR, *wznR, *wdpR, *wdnR, *wdyR;
   double rho, etaR;  // restoration: penalty, proximity weight * sqrt(mu)
   double* wsbase;    // workspace base of all scenarios (restoration re-binds from it)
@@ -410,6 +428,7 @@ struct Solver {
     dyR = gw + L.dyR; dp2R = gw + L.dp2R; dn2R = gw + L.dn2R; dy2R = gw + L.dy2R; cms = gw + L.cms;
     filtR = gw + L.filtR;
     accU = gw + L.accU; accZl = gw + L.accZl; accZu = gw + L.accZu; accY = gw + L.accY;
+    meq = 0; nneg = 0;
     wU = gw + L.wU; wzl = gw + L.wzl; wzu = gw + L.wzu; wdU = gw + L.wdU; wsl = gw + L.ws; wy = gw + L.wy;
     wvl = gw + L.wvl; wvu = gw + L.wvu; wds = gw + L.wds; wpR = gw + L.wpR; wnR = gw + L.wnR;
     wzpR = gw + L.wzpR; wznR = gw + L.wznR; wdpR = gw + L.wdpR; wdnR = gw + L.wdnR; wdyR = gw + L.wdyR;
@@ -788,6 +807,289 @@ struct Solver {
     return rr;
   }
 
+  // ------------------------------------------------ equality rows (lbg == ubg)
+  // IPOPT's c(x) = g(x) - g_l = 0: the row keeps its slot, its bounds are
+  // NaN (so every bound test sees no bound: no slack barrier, no bound multipliers, no
+  // fraction to the boundary) and its slack s is pinned at the scaled target, so d - s = c
+  // enters theta, the residuals and the filter unchanged.  The Newton step adds the
+  // equality rows through the Schur complement of the augmented system.
+  __device__ __forceinline__ static bool eqrow(double lo) { return lo != lo; }
+  // compile-time false outside the equality class; inside it the wave-uniform meq > 0
+  // test first, so a batch without equality rows skips the bound load and the select
+  __device__ __forceinline__ bool eqlo(double lo) const { return CAP::eq && meq > 0 && eqrow(lo); }
+  __device__ __forceinline__ bool eqr(int r) const { return CAP::eq && meq > 0 && eqrow(dl[r]); }
+  // equality-row workspace (indices, factored Schur complement + pivot signs, dy_c of the
+  // step / SOC), addressed off U through an opaque copy rather than held as four more
+  // pointers live across the whole solve
+  __device__ __forceinline__ GLB double* eqw(int off) const {
+    GLB double* p = U;
+    asm volatile("" : "+s"(p));
+    return p + (off - CAP::L.U);
+  }
+  __device__ __forceinline__ GLB int* eqi_() const { return (GLB int*)eqw(CAP::L.eqi); }
+  __device__ __forceinline__ GLB double* eqS_() const { return eqw(CAP::L.eqS); }
+  __device__ __forceinline__ GLB double* eqy_() const { return eqw(CAP::L.eqy); }
+  __device__ __forceinline__ GLB double* eqy2_() const { return eqw(CAP::L.eqy2); }
+  // J_r dX (scaled row Jacobian times the state step at the row's stage), as in row_step
+  __device__ __forceinline__ double row_jd(int r, const LDS double* dXs) const {
+    const int k = r / m, i = r - k * m;
+    const LDS double* xk = X + k * 8;
+    const LDS double* dxk = dXs + k * 8;
+    if (i < nb) return dc[r] * dxk[boxidx(i)];
+    const int o = i - nb;
+    const double ddx = xk[0] - obx[o], ddy = xk[1] - oby[o];
+    const double idd = rsq(ddx * ddx + ddy * ddy);
+    return dc[r] * ((-(ddx * idd)) * dxk[0] + (-(ddy * idd)) * dxk[1]);
+  }
+  // the same row's scaled state gradient (8 entries of stage r / m)
+  __device__ __forceinline__ void row_grad8(int r, double g8[8]) const {
+    const int k = r / m, i = r - k * m;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) g8[c] = 0.0;
+    const double dcr = dc[r];
+    if (i < nb) {
+      const int bi = boxidx(i);
+#pragma unroll
+      for (int c = 0; c < 8; ++c) g8[c] = (c == bi) ? dcr : 0.0;
+    } else {
+      const LDS double* xk = X + k * 8;
+      const int o = i - nb;
+      const double ddx = xk[0] - obx[o], ddy = xk[1] - oby[o];
+      const double idd = rsq(ddx * ddx + ddy * ddy);
+      g8[0] = dcr * (-(ddx * idd));
+      g8[1] = dcr * (-(ddy * idd));
+    }
+  }
+  // solve with the stored Riccati factors, signed pivots (the factorization may be
+  // indefinite when there are equality rows): ke < 0 -> the assembled linear terms (qs,
+  // rv); ke >= 0 -> the unit problem q_ke = g8, every other term 0.  Writes kf.
+  __device__ __forceinline__ void resolve_eq(const GLB double* rv, int ke, const double* g8) {
+    double p8[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) p8[i] = ke < 0 ? qs[N * 10 + i] : (ke == N ? g8[i] : 0.0);
+    for (int k = N - 1; k >= 0; --k) {
+      double E03, E04, E13, E14, E23, b00, b10, b20;
+      stage_AB(k, E03, E04, E13, E14, E23, b00, b10, b20);
+      double Lm[21], idg[6], sg[6], rt[6], v[6];
+#pragma unroll
+      for (int t = 0; t < 21; ++t) Lm[t] = Rk[k * 21 + t];
+#pragma unroll
+      for (int c = 0; c < 6; ++c) {
+        double dg = Lm[c * (c + 1) / 2 + c];
+#pragma unroll
+        for (int t = 0; t < c; ++t) dg -= (sg[t] * Lm[c * (c + 1) / 2 + t]) * Lm[c * (c + 1) / 2 + t];
+        sg[c] = dg < 0.0 ? -1.0 : 1.0;
+        dg = fabs(dg);
+        const double ig = rsq(dg);
+        Lm[c * (c + 1) / 2 + c] = dg * ig;
+        idg[c] = ig;
+#pragma unroll
+        for (int r = c + 1; r < 6; ++r) {
+          double a = Lm[r * (r + 1) / 2 + c];
+#pragma unroll
+          for (int t = 0; t < c; ++t) a -= (sg[t] * Lm[r * (r + 1) / 2 + t]) * Lm[c * (c + 1) / 2 + t];
+          Lm[r * (r + 1) / 2 + c] = (a * ig) * sg[c];
+        }
+      }
+      const bool ur = ke < 0;
+      rt[0] = (ur ? rv[k * 6 + 0] : 0.0) + ((b00 * p8[0] + b10 * p8[1]) + b20 * p8[2]);
+#pragma unroll
+      for (int r = 1; r < 6; ++r) rt[r] = (ur ? rv[k * 6 + r] : 0.0) + T * p8[2 + r];
+      if (nfix > 0) {
+        const int fm = fixm[k];
+#pragma unroll
+        for (int r = 0; r < 6; ++r)
+          if ((fm >> r) & 1) rt[r] = 0.0;
+      }
+#pragma unroll
+      for (int r = 0; r < 6; ++r) {
+        double a = rt[r];
+#pragma unroll
+        for (int t = 0; t < r; ++t) a -= Lm[r * (r + 1) / 2 + t] * v[t];
+        v[r] = a * idg[r];
+      }
+#pragma unroll
+      for (int r = 0; r < 6; ++r) v[r] *= sg[r];
+#pragma unroll
+      for (int r = 5; r >= 0; --r) {
+        double a = v[r];
+#pragma unroll
+        for (int t = r + 1; t < 6; ++t) a -= Lm[t * (t + 1) / 2 + r] * v[t];
+        v[r] = a * idg[r];
+      }
+      if (lanef() == 0) {
+#pragma unroll
+        for (int r = 0; r < 6; ++r) kf[k * 6 + r] = -v[r];
+      }
+      double pn[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        double atp = p8[i];
+        if (i == 3) atp = atp + ((E03 * p8[0] + E13 * p8[1]) + E23 * p8[2]);
+        else if (i == 4) atp = atp + (E04 * p8[0] + E14 * p8[1]);
+        double kr = 0.0;
+#pragma unroll
+        for (int r = 0; r < 6; ++r) kr += K[k * 48 + r * 8 + i] * rt[r];
+        const double qk = ur ? qs[k * 10 + i] : (k == ke ? g8[i] : 0.0);
+        pn[i] = (qk + atp) + kr;
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i) p8[i] = pn[i];
+    }
+    sync();
+  }
+  // Schur complement S = J_c H^-1 J_c^T of the equality rows from meq unit solves, and its
+  // signed Cholesky factor (lane l holds row l) with delta_c = 0, then IPOPT's
+  // jacobian_regularization_value * mu^0.25 if S is singular.  Inertia test (Haynsworth):
+  // the augmented system [H J_c^T; J_c -delta_c I] has n positive and meq negative
+  // eigenvalues iff S + delta_c I has exactly as many negative pivots as the Riccati sweep
+  // had (nneg).  The factor and the pivot signs go to eqS for the step's solves.
+  // (allow_dc false: the least-squares multipliers, which IPOPT computes without
+  // regularisation -- a singular S there means y = 0)
+  __device__ __forceinline__ bool eq_schur(double mu_, bool allow_dc = true) {
+    const int ln = lanef();
+    double row[NMPC_MEQ];
+#pragma unroll
+    for (int c = 0; c < NMPC_MEQ; ++c) row[c] = 0.0;
+    for (int e = 0; e < meq; ++e) {
+      const int re = eqi_()[e];
+      double g8[8];
+      row_grad8(re, g8);
+      resolve_eq(ru, re / m, g8);
+      forward(dUr, Xt);  // -H^-1 J_e^T (the fp64 classes' refinement buffer; Xt is free here)
+      const double se = ln < meq ? -row_jd(eqi_()[ln < meq ? ln : 0], Xt) : 0.0;
+#pragma unroll
+      for (int c = 0; c < NMPC_MEQ; ++c)
+        if (c == e) row[c] = se;
+      sync();
+    }
+    double scale = 0.0;
+#pragma unroll
+    for (int c = 0; c < NMPC_MEQ; ++c)
+      if (c < meq) scale = fmax(scale, fabs(readlane_d(row[c], c)));
+    for (int att = 0; att < (allow_dc ? 2 : 1); ++att) {
+      const double dcv = att == 0 ? 0.0 : 1e-8 * pow(mu_, 0.25);
+      double L[NMPC_MEQ], sgS[NMPC_MEQ];
+#pragma unroll
+      for (int c = 0; c < NMPC_MEQ; ++c) L[c] = row[c] + ((c == ln) ? dcv : 0.0);
+      bool sing = false;
+      int negS = 0;
+#pragma unroll
+      for (int c = 0; c < NMPC_MEQ; ++c) {
+        sgS[c] = 1.0;
+        if (c < meq) {
+          const double d = readlane_d(L[c], c);
+          if (!(fabs(d) > 1e-14 * scale)) sing = true;
+          sgS[c] = d < 0.0 ? -1.0 : 1.0;
+          negS += d < 0.0 ? 1 : 0;
+          const double ig = rsq(fabs(d));
+          const double Lcc = fabs(d) * ig;
+          L[c] = (ln == c) ? Lcc : ((ln > c) ? (L[c] * ig) * sgS[c] : L[c]);
+#pragma unroll
+          for (int c2 = c + 1; c2 < NMPC_MEQ; ++c2) {
+            if (c2 < meq) {
+              const double Lc2c = readlane_d(L[c], c2);
+              if (ln > c) L[c2] -= (L[c] * sgS[c]) * Lc2c;
+            }
+          }
+        }
+      }
+      if (sing) continue;
+      if (negS != nneg) return false;
+      if (ln < meq) {
+#pragma unroll
+        for (int c = 0; c < NMPC_MEQ; ++c) eqS_()[ln * NMPC_MEQ + c] = L[c];
+      }
+      if (ln == 0) {
+#pragma unroll
+        for (int c = 0; c < NMPC_MEQ; ++c) eqS_()[NMPC_MEQ * NMPC_MEQ + c] = sgS[c];
+      }
+      sync();
+      return true;
+    }
+    return false;
+  }
+  // dy = (S + delta_c I)^-1 rhs with the stored factor (rhs: lane e holds entry e); every
+  // lane returns the full solution in lane-e order through readlane-able registers
+  __device__ __forceinline__ double eq_solve(double rhs) const {
+    const int ln = lanef();
+    double L[NMPC_MEQ], sgS[NMPC_MEQ];
+#pragma unroll
+    for (int c = 0; c < NMPC_MEQ; ++c) {
+      L[c] = (ln < meq) ? eqS_()[(ln < meq ? ln : 0) * NMPC_MEQ + c] : 0.0;
+      sgS[c] = eqS_()[NMPC_MEQ * NMPC_MEQ + c];
+    }
+    // L z = rhs (column-oriented: lane l keeps its partial sum)
+    double part = ln < meq ? rhs : 0.0;
+    double z[NMPC_MEQ];
+#pragma unroll
+    for (int c = 0; c < NMPC_MEQ; ++c) {
+      z[c] = 0.0;
+      if (c < meq) {
+        const double Lcc = readlane_d(L[c], c);
+        z[c] = readlane_d(part, c) / Lcc;
+        if (ln > c) part -= L[c] * z[c];
+      }
+    }
+    // L^T dy = Sigma z (every lane, broadcast entries)
+    double y[NMPC_MEQ];
+#pragma unroll
+    for (int c = NMPC_MEQ - 1; c >= 0; --c) {
+      y[c] = 0.0;
+      if (c < meq) {
+        double a = sgS[c] * z[c];
+#pragma unroll
+        for (int j = c + 1; j < NMPC_MEQ; ++j)
+          if (j < meq) a -= readlane_d(L[c], j) * y[j];
+        y[c] = a / readlane_d(L[c], c);
+      }
+    }
+    double out = 0.0;
+#pragma unroll
+    for (int c = 0; c < NMPC_MEQ; ++c)
+      if (c == ln) out = y[c];
+    return out;
+  }
+  // the step with the equality rows: base solve (dUo, dXo) with the assembled terms, then
+  // dy = (S + delta_c)^-1 (c + J_c dX0), q += J_c^T dy, solve again (Newton / SOC step);
+  // for the least-squares multipliers y_c = S^-1 (-J_c w0), q -= J_c^T y_c.  dy goes to
+  // dyo[row].
+  // MODE 0: c = d - s (Newton step); 1: c = dms (second-order correction); 2: the
+  // least-squares multipliers
+  template <int MODE>
+  __device__ __forceinline__ void eq_step(const GLB double* rv, GLB double* dUo, LDS double* dXo, GLB double* dyo) {
+    const int ln = lanef();
+    const double g0[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    resolve_eq(rv, -1, g0);
+    forward(dUo, dXo);
+    const int re = eqi_()[ln < meq ? ln : 0];
+    const double jd = row_jd(re, dXo);
+    double rhs;
+    if constexpr (MODE == 0) rhs = (d[re] - s[re]) + jd;
+    else if constexpr (MODE == 1) rhs = dms[re] + jd;
+    else rhs = -jd;
+    const double dy = eq_solve(rhs);
+    if (ln < meq) dyo[re] = dy;
+    // q_k += (+-) dy_e g8_e at each row's stage (serial over the rows: rows may share a stage)
+    for (int e = 0; e < meq; ++e) {
+      const int r = eqi_()[e];
+      double g8[8];
+      row_grad8(r, g8);
+      const double de = readlane_d(dy, e) * (MODE == 2 ? -1.0 : 1.0);
+      const int k = r / m;
+      if (ln < 8) {
+        double gv = 0.0;
+#pragma unroll
+        for (int c = 0; c < 8; ++c)
+          if (c == ln) gv = g8[c];
+        qs[k * 10 + ln] += de * gv;
+      }
+      sync();
+    }
+    resolve_eq(rv, -1, g0);
+    forward(dUo, dXo);
+  }
+
   // -------------------------------------------- Riccati: stage assembly
   // Stage-parallel (lanef() = stage k) assembly of the LQ subproblem:
   //   Qs[k] = Q_k (8x8 symmetric, packed upper, 36), qs[k] = {q_k (8), S_k[0][3], S_k[0][4]}.
@@ -832,6 +1134,11 @@ struct Solver {
                           kd * mu * ((lo && !hi ? 1.0 : 0.0) - (hi && !lo ? 1.0 : 0.0));
         A = D;
         Bw = yr + D * rd + rs;
+      }
+      if (eqr(r)) {  // equality rows: no slack elimination (the Schur step adds them)
+        if (mode == SUM_LS) { A = 0.0; Bw = 0.0; }
+        else if (mode == SUM_LS_RESTO) { A = 0.5; Bw = -((rho - zpR[r]) - (rho - znR[r])) / 2.0; }
+        else if (mode == SUM_NEWTON || mode == SUM_SOC) { A = 0.0; Bw = y[r]; }
       }
       if (on) {
         if (!soc) Wr[r] = dcr * dcr * A;
@@ -922,18 +1229,24 @@ struct Solver {
   //       lanes 0..7: column j of K = -L^-T Y_j, p_k = q_k + A^T p + K^T r~;
   //       lane 8: k = -R~^{-1} r~.
   // Stores K_k, k_k and R~_k (for the gradient-only re-solve).
+  // SG: signed pivots (R~_k = L Sigma L^T, Sigma = diag(+-1)) for problems with equality
+  // rows, whose inertia test counts the negative ones (nneg); otherwise every pivot must be
+  // positive (IPOPT's inertia test for the condensed system), as before
+  template <bool SG = false>
   __device__ __forceinline__ bool riccati(const GLB double* Rd, const GLB double* rv) {
 #ifdef NMPC_STAMPS
     if (lanef() == 0) stamps[PH_RB] += 1.0;  // count factorisations
 #endif
     STAMP0();
-    const bool r = riccati_(Rd, rv);
+    const bool r = riccati_<SG>(Rd, rv);
     STAMP1(PH_RIC);
     return r;
   }
   // arithmetic in CAP::RT (the LDS exchange arrays hold RT values)
+  template <bool SG>
   __device__ __forceinline__ bool riccati_(const GLB double* Rd, const GLB double* rv) {
     using R = typename CAP::RT;
+    int negs = 0;
     // one opaque lane index for the whole sweep (every lanef() call is a fresh register copy)
     const int ln = lanef();
     const int i = ln >> 3, j = ln & 7;
@@ -1042,24 +1355,39 @@ struct Solver {
       // ---- (2)
       R rt[6];
       { STAMP0();
-        R Lm[21], idg[6];
+        R Lm[21], idg[6], sg[6];
 #pragma unroll
         for (int t = 0; t < 21; ++t) Lm[t] = Rcc[t];
 #pragma unroll
         for (int c = 0; c < 6; ++c) {
           R dg = Lm[c * (c + 1) / 2 + c];
+          if constexpr (SG) {
 #pragma unroll
-          for (int t = 0; t < c; ++t) dg -= Lm[c * (c + 1) / 2 + t] * Lm[c * (c + 1) / 2 + t];
-          if (!(dg > zr)) ok = false;
+            for (int t = 0; t < c; ++t) dg -= (sg[t] * Lm[c * (c + 1) / 2 + t]) * Lm[c * (c + 1) / 2 + t];
+            if (!(dg != zr)) ok = false;  // a zero pivot: singular
+            sg[c] = dg < zr ? (R)-1 : (R)1;
+            negs += dg < zr ? 1 : 0;
+            dg = fabs(dg);
+          } else {
+#pragma unroll
+            for (int t = 0; t < c; ++t) dg -= Lm[c * (c + 1) / 2 + t] * Lm[c * (c + 1) / 2 + t];
+            if (!(dg > zr)) ok = false;
+          }
           const R ig = rsq(dg);
           Lm[c * (c + 1) / 2 + c] = dg * ig;
           idg[c] = ig;
 #pragma unroll
           for (int r = c + 1; r < 6; ++r) {
             R v = Lm[r * (r + 1) / 2 + c];
+            if constexpr (SG) {
 #pragma unroll
-            for (int t = 0; t < c; ++t) v -= Lm[r * (r + 1) / 2 + t] * Lm[c * (c + 1) / 2 + t];
-            Lm[r * (r + 1) / 2 + c] = v * ig;
+              for (int t = 0; t < c; ++t) v -= (sg[t] * Lm[r * (r + 1) / 2 + t]) * Lm[c * (c + 1) / 2 + t];
+              Lm[r * (r + 1) / 2 + c] = (v * ig) * sg[c];
+            } else {
+#pragma unroll
+              for (int t = 0; t < c; ++t) v -= Lm[r * (r + 1) / 2 + t] * Lm[c * (c + 1) / 2 + t];
+              Lm[r * (r + 1) / 2 + c] = v * ig;
+            }
           }
         }
         rt[0] = rvs[0] + ((b00 * pc[0] + b10 * pc[1]) + b20 * pc[2]);
@@ -1084,6 +1412,10 @@ struct Solver {
           ya[r] = a * idg[r];
           yb[r] = bb * idg[r];
         }
+        if constexpr (SG) {  // S~^T R~^-1 S~ = Y^T Sigma Y, K = -L^-T Sigma Y
+#pragma unroll
+          for (int r = 0; r < 6; ++r) ya[r] *= sg[r];
+        }
         if (upper) {
           R sy = zr;
 #pragma unroll
@@ -1091,6 +1423,10 @@ struct Solver {
           const R pv = (qv + APA) - sy;
           Pn[ln] = pv;
           Pn[ji] = pv;
+        }
+        if constexpr (SG) {
+#pragma unroll
+          for (int r = 0; r < 6; ++r) yb[r] *= sg[r];
         }
         // back substitution: lanes 0..7 column ln of K, lane 8 k = -R~^-1 r~ (every lane
         // computes it: branch-free, so it overlaps with the next stage's LDS reads)
@@ -1140,6 +1476,7 @@ struct Solver {
       }
       if (!stage(k - 1, qB, rB, vB)) break;
     }
+    if constexpr (SG) nneg = __builtin_amdgcn_readfirstlane(negs);
     return ok;
   }
 
@@ -1385,7 +1722,7 @@ struct Solver {
         jd = dc[r] * ((-(ddx * idd)) * dxk[0] + (-(ddy * idd)) * dxk[1]);
       }
       const double rd = rd_is_dms ? rdsrc[r] : d[r] - s[r];
-      dso[r] = jd + rd;
+      dso[r] = eqr(r) ? 0.0 : jd + rd;  // equality rows: the slack stays at the target
     }
     STAMP1(PH_ROWSTEP);
     sync();
@@ -1412,7 +1749,7 @@ struct Solver {
         const double idd = rsq(ddx * ddx + ddy * ddy);
         jd = dcr * ((-(ddx * idd)) * dxk[0] + (-(ddy * idd)) * dxk[1]);
       }
-      const double dsr = jd + (dr - sr);
+      const double dsr = eqlo(lo) ? 0.0 : jd + (dr - sr);
       if (on) ds[r] = dsr;
       const bool hl = hasl(lo), hu = hasu(hi);
       const double gs = -(hl ? mu_ / (sr - lo) : 0.0) + (hu ? mu_ / (hi - sr) : 0.0) +
@@ -1446,6 +1783,10 @@ struct Solver {
     const double den = 1.0 / (1.0 + D * (iSp + iSn));
     Dt = D * den;
     Dr = Dt * (c + rp * iSp - rn * iSn) + rs * den;
+    if (eqr(r)) {  // equality row: no slack, the D -> infinity limit
+      Dt = 1.0 / (iSp + iSn);
+      Dr = Dt * (c + rp * iSp - rn * iSn);
+    }
   }
   __device__ __forceinline__ double dr2(int i) const {  // D_R^2 = 1/max(1,|x_R|)^2
     const double a = fmax(1.0, fabs(UR[i]));
@@ -1476,7 +1817,7 @@ struct Solver {
       const double c = soc ? cms[r] : d[r] - s[r] - pr + nr;
       const double dyv = Dt * jd + Dr;
       const double dpv = (dyv - rp) / Sp, dnv = (-dyv - rn) / Sn;
-      const double dsv = jd + c - dpv + dnv;
+      const double dsv = eqr(r) ? 0.0 : jd + c - dpv + dnv;
       if (on) { dso[r] = dsv; dpo[r] = dpv; dno[r] = dnv; dyo[r] = dyv; }
       if (!soc) {
         const double lo = dl[r], hi = du[r], sr = s[r];
@@ -1764,6 +2105,7 @@ __device__ __forceinline__ void resto_phase(const Params* __restrict__ prm, doub
   Solver<CAP> S;
   S.bind(prm, smem, ws, threadIdx.x, b);
   S.nfix = (int)S.rvars[46];
+  if constexpr (CAP::eq) S.meq = __builtin_amdgcn_readfirstlane((int)S.rvars[47]);
   S.df = io.df; S.nfilt = io.nfilt; S.nzx = io.nzx; S.nzs = io.nzs; S.delta = 0.0;
   S.mu = io.mu0; S.tau = io.tau0;
   const nmpc_options& o = prm->o;
@@ -1831,7 +2173,8 @@ __device__ __forceinline__ void resto_phase(const Params* __restrict__ prm, doub
               const double dd = sqrt(ddx * ddx + ddy * ddy);
               jd = S.dc[r] * ((-(ddx / dd)) * dxk[0] + (-(ddy / dd)) * dxk[1]);
             }
-            const double yv = ((S.vu[r] - S.vl[r]) + (rho - S.zpR[r]) - (rho - S.znR[r]) - jd) / 3.0;
+            const double yv = S.eqr(r) ? ((rho - S.zpR[r]) - (rho - S.znR[r]) - jd) / 2.0
+                                               : ((S.vu[r] - S.vl[r]) + (rho - S.zpR[r]) - (rho - S.znR[r]) - jd) / 3.0;
             S.y[r] = yv;
             ymax = fmax(ymax, fabs(yv));
           }
@@ -1919,9 +2262,10 @@ __device__ __forceinline__ void resto_phase(const Params* __restrict__ prm, doub
           const double zp = S.zpR[r], zn = S.znR[r], dr = S.d[r], sr = S.s[r], dcr = S.dc[r];
           const double lo = S.dl[r], hi = S.du[r];
           const bool hl = S.hasl(lo), hu = S.hasu(hi);
-          const double di = fmax(fabs(-yr - vlr + vur), fmax(fabs(rho - yr - zp), fabs(rho + yr - zn)));
+          const bool eq = S.eqlo(lo);
+          const double di = fmax(eq ? 0.0 : fabs(-yr - vlr + vur), fmax(fabs(rho - yr - zp), fabs(rho + yr - zn)));
           const double drr = dr - pr + nr;
-          double c1 = 0.0, c2 = 0.0;
+          double c1 = eq ? fabs(drr - sr) : 0.0, c2 = eq ? fabs(dr - sr) : 0.0;
           if (hl) { c1 = fmax(c1, lo - drr); c2 = fmax(c2, lo - dr); }
           if (hu) { c1 = fmax(c1, drr - hi); c2 = fmax(c2, dr - hi); }
           const double cl = fabs((sr - lo) * vlr), cu = fabs((hi - sr) * vur), uc = c2 / dcr;
@@ -1982,7 +2326,7 @@ __device__ __forceinline__ void resto_phase(const Params* __restrict__ prm, doub
             S.rows([&](int r, bool on) {
               const double yr = S.y[r], vlr = S.vl[r], vur = S.vu[r], zp = S.zpR[r], zn = S.znR[r];
               const double sr = S.s[r], dr = S.d[r], pr = S.pR[r], nr = S.nR[r], lo = S.dl[r], hi = S.du[r];
-              const double dv = fmax(fabs(-yr - vlr + vur), fmax(fabs(rho - yr - zp), fabs(rho + yr - zn)));
+              const double dv = fmax(S.eqlo(lo) ? 0.0 : fabs(-yr - vlr + vur), fmax(fabs(rho - yr - zp), fabs(rho + yr - zn)));
               const double cl = fabs((sr - lo) * vlr - mu_), cu = fabs((hi - sr) * vur - mu_);
               const double cp = fmax(fabs(pr * zp - mu_), fabs(nr * zn - mu_));
               const double pi = fabs(dr - sr - pr + nr);
@@ -2395,12 +2739,39 @@ __device__ __forceinline__ int solve_one(Solver<CAP>& S, const Params* __restric
   }
   S.nfix = (int)wsum(nfix_l);
   if (S.lanef() == 0) S.rvars[46] = (double)S.nfix;
-  for (int r = S.lanef(); r < ng; r += WAVE) {
-    const double lo = io.lbg[(long long)b * io.ld_lbg + r], hi = io.ubg[(long long)b * io.ld_ubg + r];
-    S.dl[r] = lo > -BIGB ? lo - fmin(cvt, brf * fmax(1.0, fabs(lo))) : -INFINITY;  // unscaled for now
-    S.du[r] = hi < BIGB ? hi + fmin(cvt, brf * fmax(1.0, fabs(hi))) : INFINITY;
-    if (lo >= hi && lo > -BIGB) invalid = true;  // equality rows not supported
-    S.dc[r] = 1.0;
+  if constexpr (!CAP::eq) {
+    for (int r = S.lanef(); r < ng; r += WAVE) {
+      const double lo = io.lbg[(long long)b * io.ld_lbg + r], hi = io.ubg[(long long)b * io.ld_ubg + r];
+      S.dl[r] = lo > -BIGB ? lo - fmin(cvt, brf * fmax(1.0, fabs(lo))) : -INFINITY;  // unscaled for now
+      S.du[r] = hi < BIGB ? hi + fmin(cvt, brf * fmax(1.0, fabs(hi))) : INFINITY;
+      // an equality row reaches a class without them only on the fp32 leg (the host sends
+      // fp64 batches with equality rows to the equality class): Invalid_Problem_Definition
+      if (lo >= hi && lo > -BIGB) invalid = true;
+      S.dc[r] = 1.0;
+    }
+  } else {
+    int meq_l = 0;
+    for (int r0 = 0; r0 < ng; r0 += WAVE) {
+      const int r = r0 + S.lanef();
+      bool eq = false;
+      if (r < ng) {
+        const double lo = io.lbg[(long long)b * io.ld_lbg + r], hi = io.ubg[(long long)b * io.ld_ubg + r];
+        S.dl[r] = lo > -BIGB ? lo - fmin(cvt, brf * fmax(1.0, fabs(lo))) : -INFINITY;  // unscaled for now
+        S.du[r] = hi < BIGB ? hi + fmin(cvt, brf * fmax(1.0, fabs(hi))) : INFINITY;
+        if (lo > hi) invalid = true;
+        // equality row (IPOPT c(x) = 0, no relaxation): NaN bounds, slack pinned at the target
+        eq = lo == hi && lo > -BIGB;
+        if (eq) { S.dl[r] = NAN; S.du[r] = NAN; S.s[r] = lo; }
+        S.dc[r] = 1.0;
+      }
+      const unsigned long long mk = __ballot(eq);
+      const int pos = meq_l + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(mk >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)mk, 0u));
+      if (eq && pos < NMPC_MEQ) S.eqi_()[pos] = r;
+      meq_l += __popcll(mk);
+    }
+    S.meq = meq_l;
+    if (meq_l > NMPC_MEQ) invalid = true;  // more equality rows than the Schur step holds
+    if (S.lanef() == 0) S.rvars[47] = (double)meq_l;
   }
   if (S.lanef() == 0) S.filt[2 * FCAP] = 0.0;
   sync();
@@ -2517,6 +2888,7 @@ __device__ __forceinline__ int solve_one(Solver<CAP>& S, const Params* __restric
       const double span = (hl && hu) ? hi - lo : INFINITY;
       if (hl) x = fmax(x, lo + fmin(skp * fmax(1.0, fabs(lo)), skf * span));
       if (hu) x = fmin(x, hi - fmin(skp * fmax(1.0, fabs(hi)), skf * span));
+      if (S.eqlo(lo)) x = S.dc[r] * S.s[r];  // equality row: pinned at the scaled target
       S.s[r] = x;
       S.vl[r] = hl ? o.bound_mult_init_val : 0.0;
       S.vu[r] = hu ? o.bound_mult_init_val : 0.0;
@@ -2531,9 +2903,20 @@ __device__ __forceinline__ int solve_one(Solver<CAP>& S, const Params* __restric
       for (int i = S.lanef(); i < nw; i += WAVE) { S.sigx[i] = 1.0; S.ru[i] = S.zl[i] - S.zu[i]; }
       S.delta = 0.0;
       S.assemble(SUM_LS, 0.0, -S.df, false);
-      S.riccati(S.sigx, S.ru);
-      S.forward(S.dU, S.dX);
-      S.refine(S.sigx, S.ru, S.dU, S.dX);
+      bool lsok = S.riccati(S.sigx, S.ru);
+      bool lsdone = false;
+      if constexpr (CAP::eq) {
+        if (S.meq > 0) {  // [I + J_d^T J_d, -J_c^T; J_c, 0] [w; y_c] = [b; 0]
+          S.nneg = 0;
+          lsok = lsok && S.eq_schur(S.mu, false);
+          if (lsok) S.template eq_step<2>(S.ru, S.dU, S.dX, S.eqy_());
+          lsdone = true;
+        }
+      }
+      if (!lsdone) {
+        S.forward(S.dU, S.dX);
+        S.refine(S.sigx, S.ru, S.dU, S.dX);
+      }
       double ymax = 0.0;
       for (int r = S.lanef(); r < ng; r += WAVE) {
         // y = bs - J wx with J wx = Gt dX
@@ -2548,13 +2931,13 @@ __device__ __forceinline__ int solve_one(Solver<CAP>& S, const Params* __restric
           const double dd = sqrt(ddx * ddx + ddy * ddy);
           jd = S.dc[r] * ((-(ddx / dd)) * dxk[0] + (-(ddy / dd)) * dxk[1]);
         }
-        const double yv = (S.vu[r] - S.vl[r]) - jd;
+        const double yv = S.eqr(r) ? S.eqy_()[r] : (S.vu[r] - S.vl[r]) - jd;
         S.y[r] = yv;
         ymax = fmax(ymax, fabs(yv));
       }
       ymax = wmax(ymax);
       sync();
-      if (!(ymax <= o.constr_mult_init_max)) {
+      if (!lsok || !(ymax <= o.constr_mult_init_max)) {
         for (int r = S.lanef(); r < ng; r += WAVE) S.y[r] = 0.0;
       }
       sync();
@@ -2615,9 +2998,10 @@ __device__ __forceinline__ int solve_one(Solver<CAP>& S, const Params* __restric
       const double yr = S.y[r], vlr = S.vl[r], vur = S.vu[r], dr = S.d[r], sr = S.s[r], dcr = S.dc[r];
       const double lo = S.dl[r], hi = S.du[r];
       const bool hl = on && S.hasl(lo), hu = on && S.hasu(hi);
-      const double g = -yr - vlr + vur;
-      if (on) dinf = fmax(dinf, fabs(g));
-      double cv = 0.0;
+      const bool eq = S.eqlo(lo);
+      const double g = -yr - vlr + vur;  // slack component (inequality rows only)
+      if (on && !eq) dinf = fmax(dinf, fabs(g));
+      double cv = eq ? fabs(dr - sr) : 0.0;
       if (hl) cv = fmax(cv, lo - dr);
       const double cl = fabs((sr - lo) * vlr);
       if (hl) cmp = fmax(cmp, cl);
@@ -2711,7 +3095,13 @@ __device__ __forceinline__ int solve_one(Solver<CAP>& S, const Params* __restric
     while (true) {
       S.delta = delta;
       S.assemble(SUM_NEWTON, S.df, S.df, true);
-      if (S.riccati(S.sigx, S.ru)) { fact_ok = true; break; }
+      bool okf;
+      if constexpr (CAP::eq) {  // equality rows: signed pivots, augmented-system inertia
+        okf = S.meq > 0 ? S.template riccati<true>(S.sigx, S.ru) && S.eq_schur(S.mu) : S.riccati(S.sigx, S.ru);
+      } else {
+        okf = S.riccati(S.sigx, S.ru);
+      }
+      if (okf) { fact_ok = true; break; }
       sync();
       if (delta == 0.0) {
         delta = (MV[2] == 0.0) ? o.first_hessian_perturbation
@@ -2725,8 +3115,14 @@ __device__ __forceinline__ int solve_one(Solver<CAP>& S, const Params* __restric
     MV[3] = delta;
     S.delta = delta;
     if (!fact_ok) { status = ST_STEP_ERR; break; }
-    S.forward(S.dU, S.dX);
-    S.refine(S.sigx, S.ru, S.dU, S.dX);
+    bool eqs = false;
+    if constexpr (CAP::eq) {
+      if (S.meq > 0) { S.template eq_step<0>(S.ru, S.dU, S.dX, S.eqy_()); eqs = true; }
+    }
+    if (!eqs) {
+      S.forward(S.dU, S.dX);
+      S.refine(S.sigx, S.ru, S.dU, S.dX);
+    }
 
     // ===== line search (BacktrackingLineSearch + FilterLSAcceptor)
     double theta_ref = 0.0, gbd = 0.0, tiny_mx = 0.0, tiny_msv = 0.0;
@@ -2854,12 +3250,12 @@ __device__ __forceinline__ int solve_one(Solver<CAP>& S, const Params* __restric
         if (S.hasu(S.xu[i])) cm += fabs((S.xu[i] - S.U[i]) * S.zu[i] - mu);
       }
       for (int r = S.lanef(); r < ng; r += WAVE) {
-        dual += fabs(-S.y[r] - S.vl[r] + S.vu[r]);
+        if (!S.eqr(r)) dual += fabs(-S.y[r] - S.vl[r] + S.vu[r]);
         prim += fabs(S.d[r] - S.s[r]);
         if (S.hasl(S.dl[r])) cm += fabs((S.s[r] - S.dl[r]) * S.vl[r] - mu);
         if (S.hasu(S.du[r])) cm += fabs((S.du[r] - S.s[r]) * S.vu[r] - mu);
       }
-      const double nn = (double)(S.nwE - S.nfix + ng);
+      const double nn = (double)(S.nwE - S.nfix + ng - (CAP::eq ? S.meq : 0));
       const double e_c = wsum(dual) / nn + (ng ? wsum(prim) / ng : 0.0) + (nc ? wsum(cm) / nc : 0.0);
       double ft, phit, tht;
       ++ls_trials;
@@ -2871,7 +3267,7 @@ __device__ __forceinline__ int solve_one(Solver<CAP>& S, const Params* __restric
       for (int r = S.lanef(); r < ng; r += WAVE) {
         double D, rs;
         S.row_rs(r, D, rs);
-        S.dms[r] = S.y[r] + a * (D * S.ds[r] + rs);  // trial y
+        S.dms[r] = S.y[r] + a * (S.eqr(r) ? S.eqy_()[r] : D * S.ds[r] + rs);  // trial y
       }
       sync();
       S.derivs(S.Xt, S.Ut);
@@ -2893,7 +3289,7 @@ __device__ __forceinline__ int solve_one(Solver<CAP>& S, const Params* __restric
         S.dv_s(r, S.ds[r], dvl, dvu);
         const double vlt = S.vl[r] + a * dvl, vut = S.vu[r] + a * dvu;
         const double sv = S.s[r] + a * S.ds[r];
-        dual2 += fabs(-S.dms[r] - vlt + vut);
+        if (!S.eqr(r)) dual2 += fabs(-S.dms[r] - vlt + vut);
         prim2 += fabs(S.dt[r] - sv);
         if (S.hasl(S.dl[r])) cm2 += fabs((sv - S.dl[r]) * vlt - mu);
         if (S.hasu(S.du[r])) cm2 += fabs((S.du[r] - sv) * vut - mu);
@@ -2983,9 +3379,15 @@ __device__ __forceinline__ int solve_one(Solver<CAP>& S, const Params* __restric
               }
               sync();
               S.assemble(SUM_SOC, S.df, S.df, true);
-              S.resolve(S.ru);
-              S.forward(S.dU2, S.dX);   // dX is free once gBD is known
-              S.refine(S.sigx, S.ru, S.dU2, S.dX);
+              bool eqs2 = false;
+              if constexpr (CAP::eq) {
+                if (S.meq > 0) { S.template eq_step<1>(S.ru, S.dU2, S.dX, S.eqy2_()); eqs2 = true; }
+              }
+              if (!eqs2) {
+                S.resolve(S.ru);
+                S.forward(S.dU2, S.dX);   // dX is free once gBD is known
+                S.refine(S.sigx, S.ru, S.dU2, S.dX);
+              }
               S.row_step(S.dX, S.dms, true, S.ds2);
               a_soc = S.frac_to_bound(tau, S.dU2, S.ds2);
               dsp = S.ds2;
@@ -3074,7 +3476,7 @@ __device__ __forceinline__ int solve_one(Solver<CAP>& S, const Params* __restric
         const double rs = -yr - S.mu * iSl + S.mu * iSu + kdm * ((hl && !hu ? 1.0 : 0.0) - (hu && !hl ? 1.0 : 0.0));
         const double dvl = hl ? S.mu * iSl - vlr - vlr * iSl * dsr : 0.0;
         const double dvu = hu ? S.mu * iSu - vur + vur * iSu * dsr : 0.0;
-        const double dyv = D * dsr + rs;
+        const double dyv = S.eqlo(lo) ? ((acc_kind == 2) ? S.eqy2_()[r] : S.eqy_()[r]) : D * dsr + rs;
         const double sn = sr + ap * dsr;
         double nvl = vlr + ad * dvl, nvu = vur + ad * dvu;
         if (hl) { const double Sn = sn - lo; nvl = fmax(fmin(nvl, ks * mu / Sn), mu / (ks * Sn)); }
@@ -3227,6 +3629,7 @@ __device__ __forceinline__ int solve_one(Solver<CAP>& S, const Params* __restric
 template <class CAP>
 __global__ __launch_bounds__(WAVE, CAP::wpe) void nmpc_solve_kernel(const Params* __restrict__ prm, int B, IO io) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
+  if (io.eqflag && ((*io.eqflag != 0) != CAP::eq)) return;  // the other class of the pair runs
   const int b = blockIdx.x;
   if (b >= B) return;
   Solver<CAP> S;
@@ -3337,6 +3740,7 @@ template <class CAP>
 __global__ __launch_bounds__(WAVE, CAP::wpe) void nmpc_closed_loop_kernel(const Params* __restrict__ prm, int B, IO io,
                                                                     Loop lp) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
+  if (io.eqflag && ((*io.eqflag != 0) != CAP::eq)) return;  // the other class of the pair runs
   // workgroups start roughly in blockIdx order, so a caller-supplied permutation sets
   // the order in which scenarios begin (an out-of-range entry is skipped)
   const int b = lp.order ? lp.order[blockIdx.x] : (int)blockIdx.x;
@@ -3415,6 +3819,7 @@ template <class CAP>
 __global__ __launch_bounds__(WAVE, CAP::wpe) void nmpc_closed_loop_sched_kernel(const Params* __restrict__ prm, int B,
                                                                           IO io, Loop lp, SchedQ q) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
+  if (io.eqflag && ((*io.eqflag != 0) != CAP::eq)) return;  // the other class of the pair runs
   const int K = lp.K;
   const int x = xcc_id();
   if (q.one_set && x != 0) return;  // test hook: only XCD 0's waves run (sets 1..7 unserved)
@@ -3528,6 +3933,19 @@ __global__ void nmpc_sched_init_kernel(int B, int K, const int* order, SchedQ q)
   if (i < B) q.done[i] = 0;
 }
 
+// equality-row gate: flag = 1 if any scenario has a row with lbg == ubg (finite), the
+// test solve_one's equality class applies; the flag is zeroed before on the same stream
+__global__ void nmpc_eq_scan_kernel(long long n, int ng, const double* lbg, long long ld_lbg, const double* ubg,
+                                    long long ld_ubg, int* flag) {
+  bool eq = false;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    const long long b = i / ng, r = i - b * ng;
+    const double lo = lbg[b * ld_lbg + r], hi = ubg[b * ld_ubg + r];
+    eq = eq || (lo == hi && lo > -BIGB);
+  }
+  if (eq) *flag = 1;
+}
+
 // completion-guard state of a one-workgroup-per-scenario launch (no queues)
 __global__ void nmpc_guard_init_kernel(int B, SchedQ q) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -3612,6 +4030,7 @@ ClassFns nmpc_class_fns_C();
 ClassFns nmpc_class_fns_A32();
 ClassFns nmpc_class_fns_C32();
 ClassFns nmpc_class_fns_D();
+ClassFns nmpc_class_fns_E();
 
 using CapA = Cap<20, 15, true>;   // BASELINE configs 2-4 (N=20, <=10 obstacles) and the reference's N=15 scripts
 using CapB = Cap<31, 21>;
@@ -3625,6 +4044,9 @@ using CapA32 = Cap<20, 15, true, float>;
 // the LDS-row classes run four scenarios per CU (160 KB of LDS): one wave per SIMD
 static_assert(CapA::L.total * 8 <= 40960 && CapA32::L.total * 8 <= 40960, "LDS-row class exceeds a quarter CU");
 using CapC32 = Cap<63, 21, false, float>;
+// equality rows (lbg == ubg): any supported shape, global rows, the Schur-complement step
+// compiled in.  Launched paired with the problem's own class behind IO::eqflag.
+using CapE = Cap<63, 21, false, double, true>;
 
 #ifdef NMPC_TU_CLASS
 template <class CAP>
@@ -3642,8 +4064,10 @@ ClassFns nmpc_class_fns_C() { return class_fns<CapC>(); }
 ClassFns nmpc_class_fns_A32() { return class_fns<CapA32>(); }
 #elif NMPC_TU_CLASS == 5
 ClassFns nmpc_class_fns_C32() { return class_fns<CapC32>(); }
-#else
+#elif NMPC_TU_CLASS == 6
 ClassFns nmpc_class_fns_D() { return class_fns<CapD>(); }
+#else
+ClassFns nmpc_class_fns_E() { return class_fns<CapE>(); }
 #endif
 #else  // host translation unit
 
@@ -3660,6 +4084,14 @@ struct nmpc_handle {
   KernFn kern = nullptr;
   LoopFn loop = nullptr;
   SchedFn sched = nullptr;
+  // the equality class, launched paired with the class above behind a device flag
+  // (fp64 handles; null for the fp32 leg and when NMPC_FORCE_CLASS picks a class)
+  KernFn kernE = nullptr;
+  LoopFn loopE = nullptr;
+  SchedFn schedE = nullptr;
+  int lds_bytesE = 0;
+  int residentE = 0;
+  int* deq = nullptr;          // the gate flag (nmpc_eq_scan_kernel)
   int resident = 0;            // closed-loop waves resident at once (occupancy x CUs)
   int* dsched = nullptr;       // step-queue scheduler state
   size_t sched_bytes = 0;
@@ -3683,7 +4115,8 @@ struct nmpc_handle {
 
 
 
-static void pick_class(const Params& P, KernFn* fn, LoopFn* lfn, SchedFn* sfn, int* lds_doubles, int* ws_doubles) {
+static bool pick_class(const Params& P, KernFn* fn, LoopFn* lfn, SchedFn* sfn, int* lds_doubles, int* ws_doubles) {
+  bool forced = false;
   ClassFns c;
   const bool fit_a = P.N <= CapA::nmax && P.m <= CapA::mmax;
   if (P.o.linear_solver_fp32) c = fit_a ? nmpc_class_fns_A32() : nmpc_class_fns_C32();
@@ -3696,8 +4129,23 @@ static void pick_class(const Params& P, KernFn* fn, LoopFn* lfn, SchedFn* sfn, i
     if (e[0] == 'B' && P.N <= CapB::nmax && P.m <= CapB::mmax && !P.o.linear_solver_fp32) c = nmpc_class_fns_B();
     if (e[0] == 'C' && !P.o.linear_solver_fp32) c = nmpc_class_fns_C();
     if (e[0] == 'D' && P.N <= CapD::nmax && P.m <= CapD::mmax && !P.o.linear_solver_fp32) c = nmpc_class_fns_D();
+    if (e[0] == 'E' && !P.o.linear_solver_fp32) c = nmpc_class_fns_E();
+    forced = e[0] != 0;
   }
   *fn = c.fn; *lfn = c.lfn; *sfn = c.sfn; *lds_doubles = c.lds_doubles; *ws_doubles = c.ws_doubles;
+  return forced;
+}
+
+// zero the gate flag and scan the batch's row bounds (stream-ordered before the pair)
+static int eq_gate(nmpc_handle* h, int B, const IO& io, hipStream_t st) {
+  const int ng = h->hp.ng;
+  const long long n = (io.ld_lbg == 0 && io.ld_ubg == 0) ? (long long)ng : (long long)B * ng;
+  if (hipMemsetAsync(h->deq, 0, sizeof(int), st) != hipSuccess) return fail(NMPC_E_HIP, "hipMemsetAsync gate");
+  const int thr = 256;
+  const long long blocks = (n + thr - 1) / thr;
+  hipLaunchKernelGGL(nmpc_eq_scan_kernel, dim3((unsigned)(blocks < 1024 ? blocks : 1024)), dim3(thr), 0, st, n, ng,
+                     io.lbg, io.ld_lbg, io.ubg, io.ld_ubg, h->deq);
+  return NMPC_OK;
 }
 
 static int ensure_ws(nmpc_handle* h, int B) {
@@ -3797,8 +4245,13 @@ int nmpc_create(const nmpc_desc* desc, nmpc_handle** out) {
   P.o = desc->opts;
   {
     int ldsd = 0;
-    pick_class(P, &h->kern, &h->loop, &h->sched, &ldsd, &h->ws_doubles);
+    const bool forced = pick_class(P, &h->kern, &h->loop, &h->sched, &ldsd, &h->ws_doubles);
     h->lds_bytes = ldsd * 8;
+    if (!P.o.linear_solver_fp32 && !forced) {
+      const ClassFns ce = nmpc_class_fns_E();
+      h->kernE = ce.fn; h->loopE = ce.lfn; h->schedE = ce.sfn; h->lds_bytesE = ce.lds_doubles * 8;
+      if (ce.ws_doubles > h->ws_doubles) h->ws_doubles = ce.ws_doubles;
+    }
   }
   if (const char* e = std::getenv("NMPC_LDS_BYTES")) {  // diagnostics: pad LDS to cap workgroups per CU
     const int want = std::atoi(e);
@@ -3820,6 +4273,16 @@ int nmpc_create(const nmpc_desc* desc, nmpc_handle** out) {
       hipFuncSetAttribute((const void*)h->sched, hipFuncAttributeMaxDynamicSharedMemorySize,
                           h->lds_bytes) != hipSuccess) {
     hipFree(h->dprm); delete h; return fail(NMPC_E_HIP, "hipFuncSetAttribute(MaxDynamicSharedMemorySize)");
+  }
+  if (h->kernE) {
+    if (hipFuncSetAttribute((const void*)h->kernE, hipFuncAttributeMaxDynamicSharedMemorySize, h->lds_bytesE) != hipSuccess ||
+        hipFuncSetAttribute((const void*)h->loopE, hipFuncAttributeMaxDynamicSharedMemorySize, h->lds_bytesE) != hipSuccess ||
+        hipFuncSetAttribute((const void*)h->schedE, hipFuncAttributeMaxDynamicSharedMemorySize, h->lds_bytesE) != hipSuccess) {
+      hipFree(h->dprm); delete h; return fail(NMPC_E_HIP, "hipFuncSetAttribute(MaxDynamicSharedMemorySize), equality class");
+    }
+    if (hipMalloc(&h->deq, sizeof(int)) != hipSuccess) {
+      hipFree(h->dprm); delete h; return fail(NMPC_E_NOMEM, "hipMalloc gate flag");
+    }
   }
   *out = h;
   return NMPC_OK;
@@ -3859,6 +4322,7 @@ int nmpc_destroy(nmpc_handle* h) {
   if (h->dws) hipFree(h->dws);
   if (h->dsched) hipFree(h->dsched);
   if (h->dtimes) hipFree(h->dtimes);
+  if (h->deq) hipFree(h->deq);
   delete h;
   return NMPC_OK;
 }
@@ -3914,6 +4378,7 @@ int nmpc_solve_batch_dev(nmpc_handle* h, int32_t B, const double* x0, int64_t ld
   io.x_out = x_out; io.f_out = f_out; io.g_out = g_out; io.lam_x = lam_x_out; io.lam_g = lam_g_out;
   io.lam_p = lam_p_out;
   io.X_out = X_out; io.status = status; io.iters = iters; io.trace = nullptr;
+  io.eqflag = h->kernE ? h->deq : nullptr;
   if (h->trace) {
     const size_t need = (size_t)B * (P.o.max_iter + 3) * TRACE_F * sizeof(double);
     if (need > h->trace_bytes) {
@@ -3928,8 +4393,14 @@ int nmpc_solve_batch_dev(nmpc_handle* h, int32_t B, const double* x0, int64_t ld
   if (int rc = ensure_ws(h, B)) return rc;
   io.ws = h->dws;
   h->last_B = B;
+  if (h->kernE) {
+    if (int rc = eq_gate(h, B, io, (hipStream_t)stream)) return rc;
+  }
   hipLaunchKernelGGL(h->kern, dim3(B), dim3(WAVE), h->lds_bytes, (hipStream_t)stream,
                      (const Params*)h->dprm, (int)B, io);
+  if (h->kernE)
+    hipLaunchKernelGGL(h->kernE, dim3(B), dim3(WAVE), h->lds_bytesE, (hipStream_t)stream,
+                       (const Params*)h->dprm, (int)B, io);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return fail(NMPC_E_HIP, std::string("kernel launch: ") + hipGetErrorString(e));
   return NMPC_OK;
@@ -4046,6 +4517,10 @@ int nmpc_closed_loop_dev(nmpc_handle* h, int32_t B, int32_t K, const double* lbx
   io.ld_lbx = ld_lbx; io.ld_ubx = ld_ubx; io.ld_lbg = ld_lbg; io.ld_ubg = ld_ubg;
   if (int rc = ensure_ws(h, B)) return rc;
   io.ws = h->dws;
+  io.eqflag = h->kernE ? h->deq : nullptr;
+  if (h->kernE) {
+    if (int rc = eq_gate(h, B, io, (hipStream_t)stream)) return rc;
+  }
   Loop lp;
   lp.K = K; lp.p = p; lp.ld_p = ld_p; lp.w = w; lp.vt = v_t; lp.wt = w_t; lp.ld_tk = ld_tk; lp.ld_tb = ld_tb;
   lp.u_hist = u_hist; lp.x_hist = x_hist; lp.f_hist = f_hist; lp.fov_hist = fov_hist;
@@ -4076,6 +4551,11 @@ int nmpc_closed_loop_dev(nmpc_handle* h, int32_t B, int32_t K, const double* lbx
       return fail(NMPC_E_HIP, "occupancy query");
     cus = prop.multiProcessorCount;
     h->resident = per_cu * cus;
+    if (h->schedE) {
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)h->schedE, WAVE, h->lds_bytesE) != hipSuccess)
+        return fail(NMPC_E_HIP, "occupancy query");
+      h->residentE = per_cu * cus;
+    }
   }
   if (h->nxcc < 0) {
     int nx = 0;
@@ -4129,6 +4609,10 @@ int nmpc_closed_loop_dev(nmpc_handle* h, int32_t B, int32_t K, const double* lbx
     }
     hipLaunchKernelGGL(h->sched, dim3(waves), dim3(WAVE), h->lds_bytes, (hipStream_t)stream,
                        (const Params*)h->dprm, (int)B, io, lp, q);
+    // the equality class on the same queues (exactly one of the pair runs)
+    if (h->schedE && h->residentE >= NXCD)
+      hipLaunchKernelGGL(h->schedE, dim3(h->residentE < waves ? h->residentE : waves), dim3(WAVE), h->lds_bytesE,
+                         (hipStream_t)stream, (const Params*)h->dprm, (int)B, io, lp, q);
     h->last_policy = 1;
     h->last_waves = waves;
   } else {
@@ -4139,6 +4623,9 @@ int nmpc_closed_loop_dev(nmpc_handle* h, int32_t B, int32_t K, const double* lbx
                        (int)B, q);
     hipLaunchKernelGGL(h->loop, dim3(B), dim3(WAVE), h->lds_bytes, (hipStream_t)stream,
                        (const Params*)h->dprm, (int)B, io, lp);
+    if (h->loopE)
+      hipLaunchKernelGGL(h->loopE, dim3(B), dim3(WAVE), h->lds_bytesE, (hipStream_t)stream,
+                         (const Params*)h->dprm, (int)B, io, lp);
   }
   // completion guard, both policies: every scenario ran its K steps, else err |= 2 and
   // the unrun steps are marked in the histories

@@ -891,7 +891,9 @@ void Solver::solve(const double* w0p, const double* p, const double* lbxp, const
   const Vec w0in(w0p, w0p + n);
   R.x.assign(n, 0.0); R.g.assign(m, 0.0); R.lam_x.assign(n, 0.0); R.lam_g.assign(m, 0.0);
   for (int r = 0; r < m; ++r) {
-    if (std::fabs(lbgp[r]) < INF && lbgp[r] == ubgp[r]) {  // equality rows: not restated (oracle raises)
+    // equality rows are restated in oracle/nmpc_oracle.py and the kernel, not here: this
+    // restatement is the bench's CPU baseline, whose workloads have none
+    if (std::fabs(lbgp[r]) < INF && lbgp[r] == ubgp[r]) {
       R.status = ST_EQ; R.iter = 0; R.x = w0in;
       return;
     }

@@ -1614,8 +1614,11 @@ def ls_mults(J, bx, bs, eq):
     K[:nx, :nx] = np.eye(nx) + Jd.T @ Jd
     K[:nx, nx:] = -Jc.T
     K[nx:, :nx] = Jc
-    sol = np.linalg.solve(K, np.concatenate([bx + Jd.T @ bs[~eq], np.zeros(nc)]))
     y = np.zeros(J.shape[0])
+    try:
+        sol = np.linalg.solve(K, np.concatenate([bx + Jd.T @ bs[~eq], np.zeros(nc)]))
+    except np.linalg.LinAlgError:  # rank-deficient J_c: IPOPT then starts from y = 0
+        return y
     y[~eq] = bs[~eq] - Jd @ sol[:nx]
     y[eq] = sol[nx:]
     return y

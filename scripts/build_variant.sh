@@ -8,7 +8,7 @@ SRC=${NMPC_SRC:-/root/repo/mpc-implementation_amd/csrc/nmpc_solve.hip}
 T=$(mktemp -d)
 F="--offload-arch=gfx950 -O3 -std=c++17 -fPIC $LICM -Wno-unused-result -Wno-unused-value $EXTRA -I /root/repo/include"
 pids=""
-for tu in HOST 1 2 3 4 5 6; do
+for tu in HOST 1 2 3 4 5 6 7; do
   if [ $tu == HOST ]; then D=-DNMPC_TU_HOST; else D=-DNMPC_TU_CLASS=$tu; fi
   /opt/rocm/bin/hipcc $F $D -c $SRC -o $T/$tu.o & pids="$pids $!"
 done

@@ -134,7 +134,10 @@ def test_closed_loop_budget_stops_cleanly(cpu):
         assert np.all(r["status"][b, r["steps"][b]:] == -1000)
 
 
-def test_equality_rows_rejected_like_the_oracle(cpu):
+def test_equality_rows_left_to_the_oracle(cpu):
+    # the compiled restatement is the bench's CPU baseline (no equality rows in its
+    # workloads): it reports -11 for them; the numpy oracle and the kernel solve them
+    # (tests/test_oracle.py, tests/test_gpu_equality.py)
     from oracle import nmpc_oracle as orc
     prob = orc.make_problem(None, N=4, T=0.2)
     lbx, ubx, lbg, ubg = orc.bounds(prob)
@@ -143,8 +146,8 @@ def test_equality_rows_rejected_like_the_oracle(cpu):
     p = np.array([0, 0, 100, 0, 0, 0, 0, 0, 50, 50, 0.0])
     r = cpu.solve_batch(prob, np.zeros((1, prob.nw)), p[None], lbx, ubx, lbg, ubg, orc.REFERENCE_OPTS)
     assert r["status"][0] == -11
-    with pytest.raises(ValueError):
-        orc.IpoptDense(prob, orc.REFERENCE_OPTS).solve(np.zeros(prob.nw), lbx, ubx, lbg, ubg, p)
+    ref = orc.IpoptDense(prob, orc.REFERENCE_OPTS).solve(np.zeros(prob.nw), lbx, ubx, lbg, ubg, p)
+    assert ref["status"] in (0, 1, 2, -1, -2, -3)
 
 
 @pytest.mark.parametrize("model", ["uav8g", "uav5"])

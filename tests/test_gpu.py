@@ -151,7 +151,7 @@ def test_invalid_inputs_reported_per_scenario():
     LG = np.repeat(lbg[:, None], 4, 1); UG = np.repeat(ubg[:, None], 4, 1)
     Pt = P.T.copy()
     LB[3, 0] = UB[3, 0] + 1.0          # lbx > ubx -> Invalid_Problem_Definition
-    LG[0, 1] = UG[0, 1] = 100.0        # equality row (unsupported) -> Invalid_Problem_Definition
+    LG[0, 1] = UG[0, 1] + 1.0          # lbg > ubg -> Invalid_Problem_Definition
     Pt[2, 2] = np.nan                  # NaN in p -> Invalid_Number_Detected
     s = _solver(spec)
     s(x0=np.zeros(spec.nw), lbx=LB, ubx=UB, lbg=LG, ubg=UG, p=Pt)
