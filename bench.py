@@ -392,8 +392,10 @@ def main():
                                     if world > 1 and args.config == 3 else "")
                                    + f"config {args.config}: batch={B}/GPU, "
                                    f"{'no-gimbal 5-state' if spec.model == 'uav5' else '8-state UAV+gimbal'}, "
-                                   f"N={spec.N}, {spec.n_obs} static obstacles"
-                                   f"{' (Race Track 2.py layout)' if spec.n_obs else ''}, T={spec.T}, "
+                                   f"N={spec.N}, {spec.n_obs} obstacles"
+                                   + (" (moving per MATLAB/Dynamic Obstacles schedule)" if pstep is not None
+                                      else " static (Race Track 2.py layout)" if spec.n_obs else "")
+                                   + f", T={spec.T}, "
                                    f"reference IPOPT opts, {mode_txt}",
                        "global_batch": B * world, "seq_len": spec.N, "parallelism": f"dp{world}"},
             "roofline": {"bound": "hbm", "achieved": achieved_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
