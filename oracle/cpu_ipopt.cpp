@@ -451,14 +451,20 @@ void add_rows(const Prob& P, const Ev& ev, const double* wr, const double* dc, d
 // inertia test (every R~_k = R_k + B^T P B positive definite).
 struct Riccati {
   int N = 0, nx = 0, nu = 0;
-  Vec K, L, idg, kv;
+  Vec K, L, idg, kv, sg;
   const char* fix = nullptr;  // fixed decision variables (make_parameter): decoupled, zero step
+  // signed pivots (problems with equality rows): R~_k = L Sigma L^T, Sigma = diag(+-1), and
+  // nneg counts the negative ones for the augmented system's inertia test (the kernel's
+  // riccati<true>); otherwise every pivot must be positive (IPOPT's inertia test)
+  bool sgn = false;
+  int nneg = 0;
   void size(const Prob& p) {
     N = p.N; nx = p.nx; nu = p.nu;
     K.assign(N * 48, 0.0);
     L.assign(N * 36, 0.0);
     idg.assign(N * 6, 0.0);
     kv.assign(N * 6, 0.0);
+    sg.assign(N * 6, 1.0);
   }
   bool factor(const Prob& Pr, const Ev& ev, const double* Q, const double* S, const double* R) {
     return nx == 8 ? factor_t<8, 6>(Pr, ev, Q, S, R) : factor_t<5, 3>(Pr, ev, Q, S, R);
@@ -476,7 +482,8 @@ struct Riccati {
   }
   // K = -R~^{-1} S~ for all NX columns at once (L L^T = R~, idg = 1 / diag L)
   template <int NX, int NU>
-  static void chol_solve_cols(const double* Lo, const double* idg, const double* Sm, double* Km) {
+  static void chol_solve_cols(const double* Lo, const double* idg, const double* Sm, double* Km,
+                              const double* sgp = nullptr) {
     double V[NU][8];
     for (int i = 0; i < NU; ++i) {
       for (int j = 0; j < NX; ++j) {
@@ -485,6 +492,9 @@ struct Riccati {
         V[i][j] = s * idg[i];
       }
     }
+    if (sgp)
+      for (int i = 0; i < NU; ++i)
+        for (int j = 0; j < NX; ++j) V[i][j] *= sgp[i];
     for (int i = NU - 1; i >= 0; --i) {
       for (int j = 0; j < NX; ++j) {
         double s = V[i][j];
@@ -512,13 +522,35 @@ struct Riccati {
     }
     return true;
   }
+  // L Sigma L^T with signed pivots (a zero pivot: singular)
   template <int NU>
-  void chol_solve_t(const double* Lo, const double* idg, double* v) const {
+  static bool chol_sg(const double* M, double* Lo, double* idg, double* sgp, int& neg) {
+    for (int i = 0; i < NU; ++i) {
+      for (int j = 0; j <= i; ++j) {
+        double s = M[i * 6 + j];
+        for (int t = 0; t < j; ++t) s -= (sgp[t] * Lo[i * 6 + t]) * Lo[j * 6 + t];
+        if (i == j) {
+          if (!(s != 0.0)) return false;
+          sgp[i] = s < 0.0 ? -1.0 : 1.0;
+          if (s < 0.0) ++neg;
+          Lo[i * 6 + i] = std::sqrt(std::fabs(s));
+          idg[i] = 1.0 / Lo[i * 6 + i];
+        } else {
+          Lo[i * 6 + j] = (s * idg[j]) * sgp[j];
+        }
+      }
+    }
+    return true;
+  }
+  template <int NU>
+  void chol_solve_t(const double* Lo, const double* idg, double* v, const double* sgp = nullptr) const {
     for (int i = 0; i < NU; ++i) {
       double s = v[i];
       for (int t = 0; t < i; ++t) s -= Lo[i * 6 + t] * v[t];
       v[i] = s * idg[i];
     }
+    if (sgp)
+      for (int i = 0; i < NU; ++i) v[i] *= sgp[i];
     for (int i = NU - 1; i >= 0; --i) {
       double s = v[i];
       for (int t = i + 1; t < NU; ++t) s -= Lo[t * 6 + i] * v[t];
@@ -529,6 +561,7 @@ struct Riccati {
   bool factor_t(const Prob& Pr, const Ev& ev, const double* Q, const double* S, const double* R) {
     alignas(32) double Pm[64], PA[64], PB[64], Rt[36], St[48], RB[48];
     for (int t = 0; t < 64; ++t) Pm[t] = Q[N * 64 + t];
+    nneg = 0;
     for (int k = N - 1; k >= 0; --k) {
       const AB ab = dyn_ab(Pr, ev.trig.data() + k * 5);
       for (int i = 0; i < NX; ++i) {  // row i of P A = A^T P[i,:]; of P B = B^T P[i,:]
@@ -557,9 +590,14 @@ struct Riccati {
           }
       double* Lk = L.data() + k * 36;
       double* ik = idg.data() + k * 6;
-      if (!chol_t<NU>(Rt, Lk, ik)) return false;
+      double* sk = sg.data() + k * 6;
+      if (sgn) {
+        if (!chol_sg<NU>(Rt, Lk, ik, sk, nneg)) return false;
+      } else if (!chol_t<NU>(Rt, Lk, ik)) {
+        return false;
+      }
       double* Kk = K.data() + k * 48;
-      chol_solve_cols<NX, NU>(Lk, ik, St, Kk);
+      chol_solve_cols<NX, NU>(Lk, ik, St, Kk, sgn ? sk : nullptr);
       if (k > 0) {  // P_k = Q_k + A^T P A + S~^T K
         double APA[64];
         for (int t = 0; t < 64; ++t) APA[t] = PA[t];
@@ -596,7 +634,7 @@ struct Riccati {
         if (fix && fix[k * NU + a]) rt[a] = 0.0;
         v[a] = rt[a];
       }
-      chol_solve_t<NU>(L.data() + k * 36, idg.data() + k * 6, v);
+      chol_solve_t<NU>(L.data() + k * 36, idg.data() + k * 6, v, sgn ? sg.data() + k * 6 : nullptr);
       for (int a = 0; a < NU; ++a) kv[k * 6 + a] = -v[a];
       if (k > 0) {  // p_k = q_k + A^T p + K^T r~
         const double* Kk = K.data() + k * 48;
@@ -710,6 +748,82 @@ class Solver {
   Vec xl, xu, dl, du, gl_, gu_, dampxl, dampxu, dampsl, dampsu, dc;
   double df = 1.0;
   int nzx = 0, nzs = 0;
+  // equality rows (lbg == ubg): IPOPT's c(x) = 0 (oracle IpoptDense, the kernel's CapE).
+  // The row keeps its slot with the slack pinned at the scaled target and no bounds; the
+  // Newton step adds the rows through the Schur complement S = J_c H^-1 J_c^T of the
+  // augmented system, from one unit solve per row with the Riccati factors.
+  static constexpr int MEQ = 16;  // the kernel's NMPC_MEQ
+  Mask eqm;
+  int neq = 0;
+  std::vector<int> eqi;
+  Vec gE;                // targets (unscaled)
+  std::vector<Vec> dxe;  // -H^-1 J_e^T per equality row
+  Vec eqL, eqSg;         // signed factor of S + delta_c I (row-major neq x neq) and pivot signs
+
+  // S from the unit solves, its signed factor with delta_c = 0, then IPOPT's
+  // jacobian_regularization_value * mu^0.25 if S is singular; inertia (Haynsworth): the
+  // augmented matrix has n positive and neq negative eigenvalues iff S + delta_c I has as
+  // many negative pivots as H had (ric.nneg).  allow_dc false: the least-squares
+  // multipliers (no regularisation; a singular S means y = 0)
+  bool eq_schur(const Ev& ev, double mu, bool allow_dc) {
+    const int mc = neq;
+    dxe.assign(mc, Vec(n, 0.0));
+    Vec S(mc * mc, 0.0), unit(m, 0.0), jd(m, 0.0), zr(n, 0.0);
+    for (int e = 0; e < mc; ++e) {
+      unit[eqi[e]] = 1.0;
+      for (int k = 0; k <= P_.N; ++k) {
+        double a[8] = {};
+        add_GT(P_, ev, k, unit.data(), dc.data(), a);
+        for (int i = 0; i < 8; ++i) qv[k * 8 + i] = a[i];
+      }
+      unit[eqi[e]] = 0.0;
+      ric.solve(P_, ev, qv.data(), zr.data(), dxe[e].data(), dXs.data());
+      jmul(P_, ev, dxe[e].data(), dc.data(), jd.data(), dXs.data());
+      for (int l = 0; l < mc; ++l) S[l * mc + e] = -jd[eqi[l]];
+    }
+    double scale = 0.0;
+    for (int c = 0; c < mc; ++c) scale = std::max(scale, std::fabs(S[c * mc + c]));
+    for (int att = 0; att < (allow_dc ? 2 : 1); ++att) {
+      const double dcv = att == 0 ? 0.0 : 1e-8 * std::pow(mu, 0.25);
+      Vec L = S, sgS(mc, 1.0);
+      for (int c = 0; c < mc; ++c) L[c * mc + c] += dcv;
+      bool sing = false;
+      int negS = 0;
+      for (int c = 0; c < mc; ++c) {  // right-looking, as the kernel's lane-per-row factor
+        const double d = L[c * mc + c];
+        if (!(std::fabs(d) > 1e-14 * scale)) sing = true;
+        sgS[c] = d < 0.0 ? -1.0 : 1.0;
+        negS += d < 0.0 ? 1 : 0;
+        const double ig = 1.0 / std::sqrt(std::fabs(d));
+        L[c * mc + c] = std::fabs(d) * ig;
+        for (int r = c + 1; r < mc; ++r) L[r * mc + c] = (L[r * mc + c] * ig) * sgS[c];
+        for (int c2 = c + 1; c2 < mc; ++c2) {
+          const double l2 = L[c2 * mc + c];
+          for (int r = c + 1; r < mc; ++r) L[r * mc + c2] -= (L[r * mc + c] * sgS[c]) * l2;
+        }
+      }
+      if (sing) continue;
+      if (negS != ric.nneg) return false;
+      eqL = L; eqSg = sgS;
+      return true;
+    }
+    return false;
+  }
+  // (S + delta_c I)^-1 rhs with the stored signed factor
+  void eq_solve(const Vec& rhs, Vec& out) const {
+    const int mc = neq;
+    Vec z(mc, 0.0), part = rhs;
+    for (int c = 0; c < mc; ++c) {
+      z[c] = part[c] / eqL[c * mc + c];
+      for (int r = c + 1; r < mc; ++r) part[r] -= eqL[r * mc + c] * z[c];
+    }
+    out.assign(mc, 0.0);
+    for (int c = mc - 1; c >= 0; --c) {
+      double a = eqSg[c] * z[c];
+      for (int j = c + 1; j < mc; ++j) a -= eqL[j * mc + c] * out[j];
+      out[c] = a / eqL[c * mc + c];
+    }
+  }
 
   void eval(const double* w, Ev& ev, bool derivs) { evaluate(P_, C, w, ev, derivs); }
   void slacks(const Vec& x, const Vec& s, Vec& Sxl, Vec& Sxu, Vec& Ssl, Vec& Ssu) const {
@@ -773,13 +887,14 @@ class Solver {
     adjoint(P_, ev, df, y.data(), dc.data(), glx.data());
     for (int i = 0; i < n; ++i) glx[i] = fixd[i] ? 0.0 : glx[i] - zl[i] + zu[i];
     gls.resize(m);
-    for (int r = 0; r < m; ++r) gls[r] = -y[r] - vl[r] + vu[r];
+    for (int r = 0; r < m; ++r) gls[r] = eqm[r] ? 0.0 : -y[r] - vl[r] + vu[r];  // slack part: inequality rows
   }
-  double cviol_scaled(const Vec& d) const {
+  double cviol_scaled(const Vec& d, const Vec& s) const {
     double c = 0.0;
     for (int r = 0; r < m; ++r) {
       if (slm[r]) c = std::max(c, std::max(0.0, dl[r] - d[r]));
       if (sum_[r]) c = std::max(c, std::max(0.0, d[r] - du[r]));
+      if (eqm[r]) c = std::max(c, std::fabs(d[r] - s[r]));
     }
     return c;
   }
@@ -789,6 +904,7 @@ class Solver {
       const double g = d[r] / dc[r];
       if (slm[r]) c = std::max(c, std::max(0.0, gl_[r] - g));
       if (sum_[r]) c = std::max(c, std::max(0.0, g - gu_[r]));
+      if (eqm[r]) c = std::max(c, std::fabs(g - gE[r]));
     }
     return c;
   }
@@ -845,9 +961,16 @@ class Solver {
   }
   // least-squares multipliers: wx = (I + w_J J^T J)^-1 (bx + J^T bsx), returns J wx
   void ls_solve(const Ev& ev, double rw, const Vec& bx_ctrl, double of, const Vec& bs, Vec& wx, Vec& jwx) {
+    ls_solve_w(ev, Vec(m, rw), bx_ctrl, of, bs, wx, jwx, nullptr);
+  }
+  // ... with per-row weights; yc: the equality rows' multipliers of
+  // [I + J_d^T W J_d, -J_c^T; J_c, 0] [wx; yc] = [b; 0] (false: singular S, y = 0)
+  bool ls_solve_w(const Ev& ev, const Vec& wr, const Vec& bx_ctrl, double of, const Vec& bs, Vec& wx, Vec& jwx,
+                  Vec* yc) {
+    ric.sgn = false;
     std::fill(Qw.begin(), Qw.end(), 0.0);
     std::fill(Sb.begin(), Sb.end(), 0.0);
-    Vec wr(m, rw), R(n, 1.0);
+    Vec R(n, 1.0);
     add_rows(P_, ev, wr.data(), dc.data(), Qw.data());
     // q_k = -(of*gl_k + G^T (dc bs)), r = -bx_ctrl
     for (int k = 0; k <= P_.N; ++k) {
@@ -863,6 +986,39 @@ class Solver {
     ric.solve(P_, ev, qv.data(), r.data(), wx.data(), dXs.data());
     jwx.assign(m, 0.0);
     jmul(P_, ev, wx.data(), dc.data(), jwx.data(), dXs.data());
+    if (!yc) return true;
+    if (!eq_schur(ev, 0.0, false)) return false;
+    Vec rhs(neq);
+    for (int e = 0; e < neq; ++e) rhs[e] = -jwx[eqi[e]];
+    eq_solve(rhs, *yc);
+    for (int e = 0; e < neq; ++e)
+      for (int i = 0; i < n; ++i) wx[i] -= (*yc)[e] * dxe[e][i];
+    jmul(P_, ev, wx.data(), dc.data(), jwx.data(), dXs.data());
+    return true;
+  }
+  // the main problem's least-squares multipliers: y = bs - J wx (inequality rows), yc
+  // (equality rows); y = 0 above ymax or when the system is singular
+  void main_ls_mults(const Ev& ev, const Vec& zl_, const Vec& zu_, const Vec& vl_, const Vec& vu_, double ymax,
+                     Vec& y) {
+    Vec bxc(n), bs(m), wx, jwx;
+    for (int i = 0; i < n; ++i) bxc[i] = -zl_[i] + zu_[i];
+    for (int r = 0; r < m; ++r) bs[r] = vu_[r] - vl_[r];
+    double ym = 0.0;
+    bool ok = true;
+    if (neq == 0) {
+      ls_solve(ev, 1.0, bxc, df, bs, wx, jwx);
+      for (int r = 0; r < m; ++r) { y[r] = bs[r] - jwx[r]; ym = std::max(ym, std::fabs(y[r])); }
+    } else {
+      Vec wr(m), yc;
+      for (int r = 0; r < m; ++r) { wr[r] = eqm[r] ? 0.0 : 1.0; if (eqm[r]) bs[r] = 0.0; }
+      ok = ls_solve_w(ev, wr, bxc, df, bs, wx, jwx, &yc);
+      if (ok) {
+        for (int r = 0; r < m; ++r) y[r] = eqm[r] ? 0.0 : bs[r] - jwx[r];
+        for (int e = 0; e < neq; ++e) y[eqi[e]] = yc[e];
+        for (int r = 0; r < m; ++r) ym = std::max(ym, std::fabs(y[r]));
+      }
+    }
+    if (!ok || ym > ymax) std::fill(y.begin(), y.end(), 0.0);
   }
 
   struct RestoOut {
@@ -890,13 +1046,14 @@ void Solver::solve(const double* w0p, const double* p, const double* lbxp, const
   }
   const Vec w0in(w0p, w0p + n);
   R.x.assign(n, 0.0); R.g.assign(m, 0.0); R.lam_x.assign(n, 0.0); R.lam_g.assign(m, 0.0);
+  eqm.assign(m, 0); eqi.clear(); gE.assign(m, 0.0);
   for (int r = 0; r < m; ++r) {
-    // equality rows are restated in oracle/nmpc_oracle.py and the kernel, not here: this
-    // restatement is the bench's CPU baseline, whose workloads have none
-    if (std::fabs(lbgp[r]) < INF && lbgp[r] == ubgp[r]) {
-      R.status = ST_EQ; R.iter = 0; R.x = w0in;
-      return;
-    }
+    if (std::fabs(lbgp[r]) < INF && lbgp[r] == ubgp[r]) { eqm[r] = 1; eqi.push_back(r); gE[r] = lbgp[r]; }
+  }
+  neq = (int)eqi.size();
+  if (neq > MEQ) {  // more equality rows than the kernel's Schur step holds: Invalid_Problem_Definition
+    R.status = ST_EQ; R.iter = 0; R.x = w0in;
+    return;
   }
   xlm.assign(n, 0); xum.assign(n, 0); slm.assign(m, 0); sum_.assign(m, 0); fixd.assign(n, 0);
   // fixed variables (lbx == ubx): IPOPT's default make_parameter -- held at the bound,
@@ -910,7 +1067,7 @@ void Solver::solve(const double* w0p, const double* p, const double* lbxp, const
     xum[i] = ubxp[i] < INF && !fixd[i];
   }
   ric.fix = fixd.data();
-  for (int r = 0; r < m; ++r) { slm[r] = lbgp[r] > -INF; sum_[r] = ubgp[r] < INF; }
+  for (int r = 0; r < m; ++r) { slm[r] = lbgp[r] > -INF && !eqm[r]; sum_[r] = ubgp[r] < INF && !eqm[r]; }
   xl = relax(lbxp, n, -1.0); xu = relax(ubxp, n, +1.0);
   gl_ = relax(lbgp, m, -1.0); gu_ = relax(ubgp, m, +1.0);
   dampxl.assign(n, 0.0); dampxu.assign(n, 0.0); dampsl.assign(m, 0.0); dampsu.assign(m, 0.0);
@@ -1010,18 +1167,11 @@ void Solver::solve(const double* w0p, const double* p, const double* lbxp, const
   Vec s(m);
   for (int r = 0; r < m; ++r) s[r] = dc[r] * ev.g[r];
   push(s, dl, du, slm, sum_, o.slack_bound_push, o.slack_bound_frac);
+  for (int e = 0; e < neq; ++e) s[eqi[e]] = dc[eqi[e]] * gE[eqi[e]];  // pinned at the scaled target
   Vec zl(n), zu(n), vl(m), vu(m), y(m, 0.0);
   for (int i = 0; i < n; ++i) { zl[i] = xlm[i] ? o.bound_mult_init_val : 0.0; zu[i] = xum[i] ? o.bound_mult_init_val : 0.0; }
   for (int r = 0; r < m; ++r) { vl[r] = slm[r] ? o.bound_mult_init_val : 0.0; vu[r] = sum_[r] ? o.bound_mult_init_val : 0.0; }
-  if (o.constr_mult_init_max > 0 && m > 0) {
-    Vec bxc(n), bs(m), wx, jwx;
-    for (int i = 0; i < n; ++i) bxc[i] = -zl[i] + zu[i];
-    for (int r = 0; r < m; ++r) bs[r] = vu[r] - vl[r];
-    ls_solve(ev, 1.0, bxc, df, bs, wx, jwx);
-    double ym = 0.0;
-    for (int r = 0; r < m; ++r) { y[r] = bs[r] - jwx[r]; ym = std::max(ym, std::fabs(y[r])); }
-    if (ym > o.constr_mult_init_max) std::fill(y.begin(), y.end(), 0.0);
-  }
+  if (o.constr_mult_init_max > 0 && m > 0) main_ls_mults(ev, zl, zu, vl, vu, o.constr_mult_init_max, y);
   double mu = o.mu_init;
   double tau = std::max(o.tau_min, 1.0 - mu);
   nzx = nzs = 0;
@@ -1064,7 +1214,7 @@ void Solver::solve(const double* w0p, const double* p, const double* lbxp, const
     err_scaling(y, zl, zu, vl, vu, sd, sc);
     grad_lag(ev, y, zl, zu, vl, vu, glx, gls);
     dinf = std::max(amax(glx), amax(gls));
-    cviol = cviol_scaled(d);
+    cviol = cviol_scaled(d, s);
     cmp = compl_max(x, s, zl, zu, vl, vu, 0.0);
     return std::max(std::max(dinf / sd, cviol), cmp / sc);
   };
@@ -1082,7 +1232,7 @@ void Solver::solve(const double* w0p, const double* p, const double* lbxp, const
                       const Vec& zu_, const Vec& vl_, const Vec& vu_, double mu_) {
     Vec gx, gs;
     grad_lag(ev_, y_, zl_, zu_, vl_, vu_, gx, gs);
-    const double dual = (sumabs(gx) + sumabs(gs)) / (nf + m);
+    const double dual = (sumabs(gx) + sumabs(gs)) / (nf + m - neq);
     double prim = 0.0;
     for (int r = 0; r < m; ++r) prim += std::fabs(d_[r] - s_[r]);
     prim = m ? prim / m : 0.0;
@@ -1163,11 +1313,15 @@ void Solver::solve(const double* w0p, const double* p, const double* lbxp, const
     Vec Rd(n);
     D.assign(m, 0.0);
     while (true) {
-      for (int r = 0; r < m; ++r) D[r] = SigS[r] + delta;
+      for (int r = 0; r < m; ++r) D[r] = eqm[r] ? 0.0 : SigS[r] + delta;  // equality rows: no slack
       for (int i = 0; i < n; ++i) Rd[i] = SigX[i] + delta;
       Qw = Qb;
       add_rows(P_, ev, D.data(), dc.data(), Qw.data());
-      if (ric.factor(P_, ev, Qw.data(), Sb.data(), Rd.data())) { fact = true; break; }
+      ric.sgn = neq > 0;  // with equality rows: signed pivots and the augmented system's inertia
+      if (ric.factor(P_, ev, Qw.data(), Sb.data(), Rd.data()) && (neq == 0 || eq_schur(ev, mu, true))) {
+        fact = true;
+        break;
+      }
       if (delta == 0.0) {
         delta = delta_last == 0.0 ? o.first_hessian_perturbation
                                   : std::max(o.min_hessian_perturbation, delta_last * o.perturb_dec_fact);
@@ -1179,11 +1333,11 @@ void Solver::solve(const double* w0p, const double* p, const double* lbxp, const
     }
     delta_curr = delta;
     if (!fact) { status = ST_STEPERR; break; }
-    for (int r = 0; r < m; ++r) D[r] = SigS[r] + delta;
+    for (int r = 0; r < m; ++r) D[r] = eqm[r] ? 0.0 : SigS[r] + delta;
     // solve_dir(rd_): uses the current y, ev (J), zl..vu (late binding as in the oracle)
     auto solve_dir = [&](const Vec& rd_, Step& st) {
       Vec v(m);
-      for (int r = 0; r < m; ++r) v[r] = y[r] + D[r] * rd_[r] + rs[r];
+      for (int r = 0; r < m; ++r) v[r] = eqm[r] ? y[r] : y[r] + D[r] * rd_[r] + rs[r];
       for (int k = 0; k <= P_.N; ++k) {
         double a[8];
         for (int i = 0; i < 8; ++i) a[i] = df * ev.gl[k * 8 + i];
@@ -1192,12 +1346,22 @@ void Solver::solve(const double* w0p, const double* p, const double* lbxp, const
       }
       ric.solve(P_, ev, qv.data(), gphib.data(), st.dx.data(), dXs.data());
       jmul(P_, ev, st.dx.data(), dc.data(), st.ds.data(), dXs.data());
+      Vec dyc;
+      if (neq) {  // [H J_c^T; J_c -delta_c I] [dx; dy_c] = [rhs; -c]: dy_c = (S + delta_c)^-1 (c + J_c dx0)
+        Vec rhs(neq);
+        for (int e = 0; e < neq; ++e) rhs[e] = rd_[eqi[e]] + st.ds[eqi[e]];
+        eq_solve(rhs, dyc);
+        for (int e = 0; e < neq; ++e)
+          for (int i = 0; i < n; ++i) st.dx[i] += dyc[e] * dxe[e][i];
+        jmul(P_, ev, st.dx.data(), dc.data(), st.ds.data(), dXs.data());
+      }
       for (int r = 0; r < m; ++r) {
-        st.ds[r] = st.ds[r] + rd_[r];
+        st.ds[r] = eqm[r] ? 0.0 : st.ds[r] + rd_[r];
         st.dy[r] = D[r] * st.ds[r] + rs[r];
         st.dvl[r] = slm[r] ? mu / Ssl[r] - vl[r] - vl[r] / Ssl[r] * st.ds[r] : 0.0;
         st.dvu[r] = sum_[r] ? mu / Ssu[r] - vu[r] + vu[r] / Ssu[r] * st.ds[r] : 0.0;
       }
+      for (int e = 0; e < neq; ++e) st.dy[eqi[e]] = dyc[e];
       for (int i = 0; i < n; ++i) {
         st.dzl[i] = xlm[i] ? mu / Sxl[i] - zl[i] - zl[i] / Sxl[i] * st.dx[i] : 0.0;
         st.dzu[i] = xum[i] ? mu / Sxu[i] - zu[i] + zu[i] / Sxu[i] * st.dx[i] : 0.0;
@@ -1495,6 +1659,7 @@ void Solver::restoration(const Vec& x0, const Vec& s0, const Vec& d0, const Ev& 
   (void)y0;
   const Opts& o = o_;
   const double rho = o.resto_penalty_parameter;
+  ric.sgn = false;  // the restoration problem's condensed matrix must be positive definite
   const Vec xR = x0;
   Vec DR2(n);
   for (int i = 0; i < n; ++i) { const double a = 1.0 / std::max(1.0, std::fabs(xR[i])); DR2[i] = a * a; }
@@ -1522,7 +1687,8 @@ void Solver::restoration(const Vec& x0, const Vec& s0, const Vec& d0, const Ev& 
   Vec dR = d0;
   auto eta = [&](double mu_) { return o.resto_proximity_weight * std::sqrt(mu_); };
   // least-squares multipliers of the restoration NLP; Jfull = [J, -I, I] with the
-  // p, n blocks eliminated: (I + J^T J / 3) wx = bx_x + J^T (bs + (bx_p - bs - bx_n - bs) / 3)
+  // p, n blocks eliminated: (I + J^T J / 3) wx = bx_x + J^T (bs + (bx_p - bs - bx_n - bs) / 3);
+  // an equality row has no slack, so two eliminated blocks: weight 1/2, y = comb - J wx / 2
   Vec yR(m, 0.0);
   if (o.constr_mult_init_max > 0 && m > 0) {
     Vec bxx(n), bs(m), comb(m), wx, jwx;
@@ -1530,14 +1696,20 @@ void Solver::restoration(const Vec& x0, const Vec& s0, const Vec& d0, const Ev& 
     for (int r = 0; r < m; ++r) {
       bs[r] = vuR[r] - vlR[r];
       const double rp_ = (rho - zp[r]) - bs[r], rn_ = (rho - zn[r]) + bs[r];
-      comb[r] = bs[r] + (rp_ - rn_) / 3.0;
+      comb[r] = eqm[r] ? ((rho - zp[r]) - (rho - zn[r])) / 2.0 : bs[r] + (rp_ - rn_) / 3.0;
     }
-    ls_solve(evR, 1.0 / 3.0, bxx, 0.0, comb, wx, jwx);
+    if (neq == 0) {
+      ls_solve(evR, 1.0 / 3.0, bxx, 0.0, comb, wx, jwx);
+    } else {
+      Vec wr(m);
+      for (int r = 0; r < m; ++r) wr[r] = eqm[r] ? 0.5 : 1.0 / 3.0;
+      ls_solve_w(evR, wr, bxx, 0.0, comb, wx, jwx, nullptr);
+    }
     double ym = 0.0;
     for (int r = 0; r < m; ++r) {
       const double rp_ = (rho - zp[r]) - bs[r], rn_ = (rho - zn[r]) + bs[r];
       const double wp = (2 * rp_ + rn_ + jwx[r]) / 3.0, wn = (rp_ + 2 * rn_ - jwx[r]) / 3.0;
-      yR[r] = bs[r] - (jwx[r] - wp + wn);
+      yR[r] = eqm[r] ? comb[r] - jwx[r] / 2.0 : bs[r] - (jwx[r] - wp + wn);
       ym = std::max(ym, std::fabs(yR[r]));
     }
     if (ym > o.constr_mult_init_max) std::fill(yR.begin(), yR.end(), 0.0);
@@ -1583,7 +1755,7 @@ void Solver::restoration(const Vec& x0, const Vec& s0, const Vec& d0, const Ev& 
     for (int i = 0; i < n; ++i)
       if (!fixd[i]) dinf = std::max(dinf, std::fabs(et * DR2[i] * (xx[i] - xR[i]) + tmpn[i] - zlR[i] + zuR[i]));
     for (int r = 0; r < m; ++r) {
-      dinf = std::max(dinf, std::fabs(-yR[r] - vlR[r] + vuR[r]));
+      if (!eqm[r]) dinf = std::max(dinf, std::fabs(-yR[r] - vlR[r] + vuR[r]));
     }
     for (int r = 0; r < m; ++r) dinf = std::max(dinf, std::fabs(rho - yR[r] - zp[r]));
     for (int r = 0; r < m; ++r) dinf = std::max(dinf, std::fabs(rho + yR[r] - zn[r]));
@@ -1592,6 +1764,7 @@ void Solver::restoration(const Vec& x0, const Vec& s0, const Vec& d0, const Ev& 
       const double dr = dR[r] - pp[r] + nn[r];
       if (slm[r]) cv = std::max(cv, std::max(0.0, dl[r] - dr));
       if (sum_[r]) cv = std::max(cv, std::max(0.0, dr - du[r]));
+      if (eqm[r]) cv = std::max(cv, std::fabs(dr - ss[r]));
       pinf = std::max(pinf, std::fabs(dR[r] - ss[r] - pp[r] + nn[r]));
     }
     double cm = compl_max(xx, ss, zlR, zuR, vlR, vuR, mu_c);
@@ -1769,7 +1942,8 @@ void Solver::restoration(const Vec& x0, const Vec& s0, const Vec& d0, const Ev& 
       for (int r = 0; r < m; ++r) {
         const double D_ = SigS[r] + delta_;
         const double spd = Sp[r] + delta_, snd = Sn[r] + delta_;
-        Dw[r] = D_ / (1.0 + D_ * (1.0 / spd + 1.0 / snd));
+        // equality rows (no slack): the D -> infinity limit
+        Dw[r] = eqm[r] ? 1.0 / (1.0 / spd + 1.0 / snd) : D_ / (1.0 + D_ * (1.0 / spd + 1.0 / snd));
       }
       for (int i = 0; i < n; ++i) Rd[i] = et * DR2[i] + (SigX[i] + delta_);
       Qw = Qb;
@@ -1791,6 +1965,7 @@ void Solver::restoration(const Vec& x0, const Vec& s0, const Vec& d0, const Ev& 
       Snd[r] = Sn[r] + delta_;
       den[r] = 1.0 / (1.0 + D_ * (1.0 / Spd[r] + 1.0 / Snd[r]));
       Dt[r] = D_ * den[r];
+      if (eqm[r]) { den[r] = 0.0; Dt[r] = 1.0 / (1.0 / Spd[r] + 1.0 / Snd[r]); }
     }
     // rdir(c_): late-bound yR, evR, zlR..zn, pp, nn (as the oracle's closure)
     auto rdir = [&](const Vec& c_, RStep& st) {
@@ -1810,7 +1985,7 @@ void Solver::restoration(const Vec& x0, const Vec& s0, const Vec& d0, const Ev& 
         st.dy[r] = Dt[r] * jd[r] + Dr[r];
         st.dp[r] = (st.dy[r] - rp[r]) / Spd[r];
         st.dn[r] = (-st.dy[r] - rn[r]) / Snd[r];
-        st.ds[r] = jd[r] + c_[r] - st.dp[r] + st.dn[r];
+        st.ds[r] = eqm[r] ? 0.0 : jd[r] + c_[r] - st.dp[r] + st.dn[r];  // linearised d(x) - s - p + n = 0
         st.dvl[r] = slm[r] ? muR / Ssl[r] - vlR[r] - vlR[r] / Ssl[r] * st.ds[r] : 0.0;
         st.dvu[r] = sum_[r] ? muR / Ssu[r] - vuR[r] + vuR[r] / Ssu[r] * st.ds[r] : 0.0;
         st.dzp[r] = muR / pp[r] - zp[r] - Sp[r] * st.dp[r];
@@ -2032,15 +2207,8 @@ void Solver::restoration(const Vec& x0, const Vec& s0, const Vec& d0, const Ev& 
     for (int r = 0; r < m; ++r) { out.vl[r] = slm[r] ? 1.0 : 0.0; out.vu[r] = sum_[r] ? 1.0 : 0.0; }
   }
   out.y.assign(m, 0.0);
-  if (o.constr_mult_reset_threshold > 0 && m > 0) {
-    Vec bxc(n), bs(m), wx, jwx;
-    for (int i = 0; i < n; ++i) bxc[i] = -out.zl[i] + out.zu[i];
-    for (int r = 0; r < m; ++r) bs[r] = out.vu[r] - out.vl[r];
-    ls_solve(evR, 1.0, bxc, df, bs, wx, jwx);
-    double ym = 0.0;
-    for (int r = 0; r < m; ++r) { out.y[r] = bs[r] - jwx[r]; ym = std::max(ym, std::fabs(out.y[r])); }
-    if (ym > o.constr_mult_reset_threshold) std::fill(out.y.begin(), out.y.end(), 0.0);
-  }
+  if (o.constr_mult_reset_threshold > 0 && m > 0)
+    main_ls_mults(evR, out.zl, out.zu, out.vl, out.vu, o.constr_mult_reset_threshold, out.y);
   out.status = ST_NONE;
   out.it = it_;
   out.x = xx;
