@@ -246,7 +246,8 @@ const char* nmpc_last_error(void);
 
 /* Diagnostics: with NMPC_STEP_TIMES set in the environment, nmpc_closed_loop_dev records
  * for every (step k, scenario b) the s_memrealtime stamps (100 MHz) at the start and end
- * of the step and the running wave (XCC_ID | workgroup << 8), K x B x 3 uint64; this
+ * of the step and the running wave with the step's shader-clock cycles (s_memtime):
+ * XCC_ID | workgroup << 8 | cycles << 24, K x B x 3 uint64; this
  * copies the last launch's record to host_out (n >= 3 K B). */
 int nmpc_closed_loop_times(nmpc_handle* h, uint64_t* host_out, int64_t n);
 

@@ -3746,11 +3746,12 @@ __global__ __launch_bounds__(WAVE, CAP::wpe) void nmpc_closed_loop_kernel(const 
   const int b = lp.order ? lp.order[blockIdx.x] : (int)blockIdx.x;
   if (b < 0 || b >= B) return;
   for (int k = 0; k < lp.K; ++k) {
-    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime(), c0 = __builtin_amdgcn_s_memtime();
     cl_step<CAP>(prm, B, io, lp, b, k, smem);
     if (lp.times && threadIdx.x == 0) {
       unsigned long long* t = lp.times + ((long long)k * B + b) * 3;
-      t[0] = t0; t[1] = __builtin_amdgcn_s_memrealtime(); t[2] = blockIdx.x;
+      t[0] = t0; t[1] = __builtin_amdgcn_s_memrealtime();
+      t[2] = (unsigned long long)blockIdx.x << 8 | (__builtin_amdgcn_s_memtime() - c0) << 24;  // + shader cycles
     }
     // completion guard (nmpc_sched_check_kernel): a duplicated or missing dispatch
     // entry leaves some scenario short of its K steps, which the check reports
@@ -3877,11 +3878,13 @@ __global__ __launch_bounds__(WAVE, CAP::wpe) void nmpc_closed_loop_sched_kernel(
     int its = 0;
     if (cb >= 0 && cb < B) {  // an out-of-range dispatch entry is claimed and skipped
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // the previous step's p, w (L1 invalidated)
-      const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+      const unsigned long long t0 = __builtin_amdgcn_s_memrealtime(), c0 = __builtin_amdgcn_s_memtime();
       its = cl_step<CAP>(prm, B, io, lp, cb, ck, smem);
       if (lp.times && threadIdx.x == 0) {
         unsigned long long* t = lp.times + ((long long)ck * B + cb) * 3;
-        t[0] = t0; t[1] = __builtin_amdgcn_s_memrealtime(); t[2] = (unsigned long long)(x | (blockIdx.x << 8));
+        t[0] = t0; t[1] = __builtin_amdgcn_s_memrealtime();
+        // XCC_ID | workgroup << 8 | shader-clock cycles of the step << 24 (effective clock)
+        t[2] = (unsigned long long)(x | (blockIdx.x << 8)) | (__builtin_amdgcn_s_memtime() - c0) << 24;
       }
       if (threadIdx.x == 0) q.done[cb] = ck + 1;
       stores_done();  // this step's p, w, histories are in the XCD's L2

@@ -1649,7 +1649,6 @@ def eq_kkt(M, Jc, mu, reg_value=1e-8, reg_exponent=0.25):
             return None
         return np.block([[M, Jc.T], [Jc, -dcv * np.eye(mc)]])
     return None
-    return None
 
 
 # --- closed loop (immediate caller, Python/NMPC_TT.py:13-30, :346-402) --------

@@ -49,6 +49,11 @@ for b in top:
 per_it = (en - st) / 1e2 / np.maximum(it, 1)  # us per iteration of every step
 print(f"us per iteration: all steps mean {np.average(per_it, weights=it):.1f}; steps with 100 iterations "
       f"{per_it[it >= 100].mean():.1f}")
+# effective shader clock per step: s_memtime cycles (t[2] >> 24) over the realtime span
+cyc = (t[:, :, 2] >> 24).astype(np.float64)
+mhz = cyc / np.maximum(en - st, 1) * 100.0
+print(f"effective shader clock per step (MHz): mean {np.average(mhz, weights=en - st):.0f}, "
+      f"p1 {np.percentile(mhz, 1):.0f}, p99 {np.percentile(mhz, 99):.0f}")
 # steps in flight over time
 edges = np.arange(0, span + 10, 10.0)
 inflight = []
@@ -67,7 +72,8 @@ print("last scenario per step: iterations / start ms / duration ms / gap before 
 prev = 0.0
 for k in range(K):
     s0, e0 = (st[k, b] - t0) / 1e5, (en[k, b] - t0) / 1e5
-    print(f"  k={k:2d} it={it[k, b]:3d} start={s0:7.1f} dur={e0 - s0:6.1f} gap={s0 - prev:6.1f} status={h['status'][k, b].item()}")
+    print(f"  k={k:2d} it={it[k, b]:3d} start={s0:7.1f} dur={e0 - s0:6.1f} gap={s0 - prev:6.1f} "
+          f"status={h['status'][k, b].item()} clock={mhz[k, b]:.0f} MHz")
     prev = e0
 wait = last - first - busy
 b = int(np.argmax(wait))
@@ -76,5 +82,5 @@ prev = None
 for k in range(K):
     s0, e0 = (st[k, b] - t0) / 1e5, (en[k, b] - t0) / 1e5
     print(f"  k={k:2d} it={it[k, b]:3d} start={s0:7.1f} dur={e0 - s0:6.1f} gap={(s0 - prev) if prev is not None else 0:6.1f} "
-          f"wave={int(t[k, b, 2]) >> 8} xcc={int(t[k, b, 2]) & 255}")
+          f"wave={(int(t[k, b, 2]) >> 8) & 0xFFFF} xcc={int(t[k, b, 2]) & 255}")
     prev = e0
