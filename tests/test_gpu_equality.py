@@ -68,3 +68,85 @@ def test_too_many_equality_rows_is_invalid_problem():
     p = np.array([90, 150, 80, 0, 0, 0, 0, 0, 100, 150, 0.0])
     _, st = _gpu_solve("nmpc_tt", 20, 1.0, np.zeros(prob.nw), lbx, ubx, lbg, ubg, p)
     assert int(np.ravel(st["status_code"])[0]) == -11
+
+
+def test_mixed_batch_with_per_scenario_bounds_matches_oracle():
+    """Per-scenario bounds (ld_lbg > 0): scenario 0 has a pinned row, scenario 1 none.  The
+    batch runs on the equality class (the device flag is batch-wide), whose path for a
+    scenario without equality rows is the ordinary one: both match the oracle."""
+    prob, p0, lbx, ubx, lbg0, ubg0, row = _pinned_z_problem(0)
+    _, p1, _, _, lbg1, ubg1, _ = _pinned_z_problem(1)
+    lbg1, ubg1 = orc.bounds(prob)[2:]
+    P = np.stack([p0, p1], axis=1)
+    LG, UG = np.stack([lbg0, lbg1], axis=1), np.stack([ubg0, ubg1], axis=1)
+    sol, st = _gpu_solve("race_track_2", 8, 0.2, np.zeros((prob.nw, 2)), lbx, ubx, LG, UG, P)
+    for b, (lg, ug, p) in enumerate(((lbg0, ubg0, p0), (lbg1, ubg1, p1))):
+        ref = orc.IpoptDense(prob, orc.REFERENCE_OPTS).solve(np.zeros(prob.nw), lbx, ubx, lg, ug, p)
+        print(f"scenario {b}: GPU {int(st['status_code'][b])} / {int(st['iter_count'][b])} iterations, "
+              f"oracle {ref['status']} / {ref['iter']}")
+        assert int(st["status_code"][b]) == ref["status"]
+        assert _rel(sol["x"][:, b], ref["x"]) <= TOL
+
+
+def test_fp32_leg_rejects_equality_rows():
+    # the fp32 Riccati leg has no equality class: Invalid_Problem_Definition (-11)
+    from nmpc_amd import nlpsol, make_spec, REFERENCE_OPTS
+    prob, p, lbx, ubx, lbg, ubg, row = _pinned_z_problem(0)
+    s = nlpsol("solver", "ipopt", make_spec("race_track_2", N=8, T=0.2),
+               dict(REFERENCE_OPTS, linear_solver_precision="single"))
+    s(x0=np.zeros(prob.nw), lbx=lbx, ubx=ubx, lbg=lbg, ubg=ubg, p=p)
+    assert int(np.ravel(s.stats()["status_code"])[0]) == -11
+
+
+@pytest.mark.parametrize("extra", [0, 173])
+def test_equality_rows_closed_loop_matches_per_step_launches(extra):
+    """nmpc_closed_loop_dev with an equality row in the shared bounds runs the equality
+    class's closed-loop kernels (one workgroup per scenario, and -- with more scenarios than
+    the problem class's resident waves -- the step queues); its histories equal K rounds of
+    solve_batch_dev + shift_dev, which run the equality class's solve kernel."""
+    import torch
+    from nmpc_amd import nlpsol, make_spec, draw_scenarios, REFERENCE_OPTS
+    spec = make_spec("race_track_2", N=8, T=0.2)
+    s = nlpsol("solver", "ipopt", spec, REFERENCE_OPTS)
+    f64 = dict(dtype=torch.float64, device="cuda")
+    lbx, ubx, lbg, ubg = (np.array(v, float) for v in spec.bounds())
+    if extra:
+        P0 = draw_scenarios(spec, 8, seed=5)
+        s.closed_loop_device(1, *[torch.tensor(v, **f64) for v in (lbx, ubx, lbg, ubg)], torch.tensor(P0, **f64),
+                             torch.zeros(8, spec.nw, **f64),
+                             torch.full((8,), 12.0, **f64), torch.full((8,), 0.01, **f64))
+        torch.cuda.synchronize()
+    B = (s.closed_loop_info()["resident_waves"] + extra) if extra else 48
+    K = 3
+    P = draw_scenarios(spec, B, seed=21)
+    # per-scenario bounds (ld_lbg = ng): z at stage 6 pinned 0.5 m above the scenario's start
+    LG, UG = np.tile(lbg, (B, 1)), np.tile(ubg, (B, 1))
+    LG[:, 6 * spec.m] = UG[:, 6 * spec.m] = P[:, 2] + 0.5
+    bnd = [torch.tensor(lbx, **f64), torch.tensor(ubx, **f64), torch.tensor(LG, **f64), torch.tensor(UG, **f64)]
+    vt, wt = torch.full((B,), 12.0, **f64), torch.full((B,), 0.01, **f64)
+    p1, w1 = torch.tensor(P, **f64), torch.zeros(B, spec.nw, **f64)
+    out = {"x": torch.empty(B, spec.nw, **f64), "f": torch.empty(B, **f64),
+           "status": torch.empty(B, dtype=torch.int32, device="cuda"),
+           "iters": torch.empty(B, dtype=torch.int32, device="cuda")}
+    ref = {"u": [], "f": [], "status": [], "iters": []}
+    for _ in range(K):
+        s.solve_device(w1, *bnd, p1, out)
+        ref["u"].append(out["x"][:, :6].clone())
+        for k in ("f", "status", "iters"):
+            ref[k].append(out[k].clone())
+        s.shift_device(p1, out["x"], w1, vt, wt)
+    p2, w2 = torch.tensor(P, **f64), torch.zeros(B, spec.nw, **f64)
+    hist = {"u": torch.empty(K, B, 6, **f64), "f": torch.empty(K, B, **f64),
+            "status": torch.empty(K, B, dtype=torch.int32, device="cuda"),
+            "iters": torch.empty(K, B, dtype=torch.int32, device="cuda")}
+    s.closed_loop_device(K, *bnd, p2, w2, vt, wt, hist)
+    torch.cuda.synchronize()
+    info = s.closed_loop_info()
+    assert info["policy"] == ("step_queues" if extra else "per_scenario")
+    st = hist["status"].cpu().numpy()
+    print(f"B={B}: statuses {dict(zip(*np.unique(st, return_counts=True)))}")
+    assert np.any(st == 0)
+    for k in ("status", "iters"):
+        np.testing.assert_array_equal(hist[k].cpu().numpy(), torch.stack(ref[k]).cpu().numpy(), err_msg=k)
+    for k in ("u", "f"):
+        assert _rel(hist[k].cpu().numpy(), torch.stack(ref[k]).cpu().numpy()) <= 1e-12, k
