@@ -111,7 +111,7 @@ constexpr Lay make_layout(int N, int m, bool lr, bool refine, bool eq) {
     L.s = g; g += al8(ng); L.y = g; g += al8(ng); L.vl = g; g += al8(ng); L.vu = g; g += al8(ng);
     L.d = g; g += al8(ng); L.ds = g; g += al8(ng); L.ds2 = g; g += al8(ng); L.dc = g; g += al8(ng);
     // the row bounds go with the rows: in the workspace for the global-row classes, whose
-    // LDS then holds only per-stage data (config 5's N = 50 class fits 5 scenarios per CU)
+    // LDS then holds only per-stage data (config 5's N = 50 class fits 6 scenarios per CU)
     L.dl = g; g += al8(ng); L.du = g; g += al8(ng);
   }
   // trial row values: in LDS with the hot rows (not in the refinement classes, whose
@@ -137,13 +137,17 @@ constexpr Lay make_layout(int N, int m, bool lr, bool refine, bool eq) {
     L.eqi = g; g += al8(NMPC_MEQ / 2 + 1); L.eqS = g; g += al8(NMPC_MEQ * NMPC_MEQ + NMPC_MEQ);
     L.eqy = g; g += al8(ng); L.eqy2 = g; g += al8(ng);
   }
+  if (!lr) { L.kf = g; g += al8(6 * N); }
   L.wstotal = g;
   L.X = o; o += al2(nX); L.Xt = o; o += al2(nX); L.dX = o; o += al2(nX);
   L.trig = o; o += al2(8 * NS); L.qs = o; o += al2(10 * NS); L.lam = o; o += al2(8 * NS);
-  L.kf = o; o += al2(6 * N); L.Rc = o; o += 22; L.Rv = o; o += 8;
+  // the Riccati feed-forward terms k_k: in LDS for the LDS-row class, in the workspace
+  // otherwise (the global-row classes' LDS then fits 6 scenarios per CU at N = 50)
+  if (lr) { L.kf = o; o += al2(6 * N); }
+  L.Rc = o; o += 22; L.Rv = o; o += 8;
   // the Riccati sweep's P / p double buffers: inside `inc` (rollout / adjoint scratch,
-  // never live during the sweep) for the LDS-row classes, separate otherwise
-  const bool pin = lr && 8 * NS >= 144;
+  // never live during the sweep) whenever it is large enough (N >= 17)
+  const bool pin = 8 * NS >= 144;
   if (!pin) { L.P0 = o; o += 64; L.P1 = o; o += 64; L.pv0 = o; o += 8; L.pv1 = o; o += 8; }
   L.St = o; o += 48;
   L.p = o; o += 64; L.ob = o; o += al2(2 * NMPC_MAX_OBS); L.inc = o; o += al2(8 * NS);
@@ -387,7 +391,9 @@ struct Solver {
   GLB double* gl, *Hl, *Qs;
   LDS double* trig, *qs, *lam;
   GLB double* K, *Rk;
-  LDS double* kf, *Rc, *Rv, *Pa, *Pb, *pva, *pvb, *St;
+  using KFT = std::conditional_t<CAP::lds_rows, LDS double, GLB double>;
+  KFT* kf;  // k_k: LDS for the LDS-row class, workspace otherwise
+  LDS double* Rc, *Rv, *Pa, *Pb, *pva, *pvb, *St;
   LDS double* pp, *obx, *oby, *inc, *stamps;
   GLB double* filt;
   LDS int* fixm;  // fixed decision variables (lbx == ubx, make_parameter): bit c of stage k
@@ -434,7 +440,9 @@ struct Solver {
     wzpR = gw + L.wzpR; wznR = gw + L.wznR; wdpR = gw + L.wdpR; wdnR = gw + L.wdnR; wdyR = gw + L.wdyR;
     gl = gw + L.gl; Hl = gw + L.Hl; trig = sm + L.trig; Qs = gw + L.Qs; qs = sm + L.qs;
     lam = sm + L.lam;
-    K = gw + L.K; kf = sm + L.kf; Rk = gw + L.Rk; Rc = sm + L.Rc; Rv = sm + L.Rv;
+    K = gw + L.K; Rk = gw + L.Rk; Rc = sm + L.Rc; Rv = sm + L.Rv;
+    if constexpr (CAP::lds_rows) kf = (KFT*)(sm + L.kf);
+    else kf = (KFT*)(gw + L.kf);
     Pa = sm + L.P0; Pb = sm + L.P1; pva = sm + L.pv0; pvb = sm + L.pv1;
     St = sm + L.St;
     pp = sm + L.p; obx = sm + L.ob; oby = obx + NMPC_MAX_OBS; inc = sm + L.inc;
@@ -4038,10 +4046,10 @@ ClassFns nmpc_class_fns_E();
 using CapA = Cap<20, 15, true>;   // BASELINE configs 2-4 (N=20, <=10 obstacles) and the reference's N=15 scripts
 using CapB = Cap<31, 21>;
 using CapC = Cap<63, 21>;   // any supported shape
-// BASELINE config 5 (N = 50, 10 obstacles): global rows and row bounds, 29 KB of LDS per
-// scenario, so 5 scenarios per CU (class C's 36 KB allows 4; before the row bounds left
-// LDS, 57 KB allowed 2)
+// BASELINE config 5 (N = 50, 10 obstacles): global rows, row bounds and k_k, 25.6 KB of
+// LDS per scenario, so 6 scenarios per CU (round 3: 57 KB allowed 2, then 29 KB 5)
 using CapD = Cap<50, 15>;
+static_assert(CapD::L.total * 8 <= 163840 / 6, "config 5's class no longer fits 6 scenarios per CU");
 // fp32 Riccati factorisation (nmpc_options.linear_solver_fp32; BASELINE config 5's fp32 leg)
 using CapA32 = Cap<20, 15, true, float>;
 // the LDS-row classes run four scenarios per CU (160 KB of LDS): one wave per SIMD
