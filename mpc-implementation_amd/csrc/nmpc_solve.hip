@@ -459,12 +459,17 @@ struct Solver {
   // X[:,0] = p[0:8]; X[:,k+1] = X[:,k] + T f(X[:,k],U[:,k])   (NMPC_TT.py:160-167)
   // Each lanef() k sums the increments j<k in order, i.e. bitwise the sequential
   // recursion; the (x,y,z) increments need theta_j, psi_j, so two passes.
-  __device__ __forceinline__ void rollout(const GLB double* Us, LDS double* Xd) {
+  // (dUs non-null: the controls are Us + a dUs, formed here from the two vectors rather
+  // than read back from the trial point just stored -- the same doubles)
+  __device__ __forceinline__ void rollout(const GLB double* Us, LDS double* Xd, const GLB double* dUs = nullptr,
+                                          double a_ = 0.0) {
     STAMP0();
     const int k = lanef();
+    auto uk = [&](int j) { return dUs ? Us[j] + a_ * dUs[j] : Us[j]; };
+    const double v = k < N ? uk(k * 6) : 0.0;
     if (k < N) {
 #pragma unroll
-      for (int c = 0; c < 5; ++c) inc[k * 8 + c] = T * Us[k * 6 + 1 + c];
+      for (int c = 0; c < 5; ++c) inc[k * 8 + c] = T * uk(k * 6 + 1 + c);
     }
     sync();
     double a[5];
@@ -480,7 +485,6 @@ struct Solver {
         }
       }
       if (k < N) {
-        const double v = Us[k * 6];
         const double ct = cos(a[0]), st_ = sin(a[0]), cp = cos(a[1]), sp = sin(a[1]);
         inc[k * 8 + 5] = T * (v * cp * ct);
         inc[k * 8 + 6] = T * (v * sp * ct);
@@ -779,13 +783,16 @@ struct Solver {
   // iteration's reference value (same slacks bit for bit: U <- Ut, s <- s + a ds)
   // per-lane partial sums: the control terms first, then the rows in rows() order
   __device__ __forceinline__ void barrier_ctrl(const GLB double* u, double& logs, double& damp) const {
-    for (int i = lanef(); i < nw; i += WAVE) {
-      const bool lo = hasl(xl[i]), hi = hasu(xu[i]);
-      if (lo) logs += log(u[i] - xl[i]);
-      if (hi) logs += log(xu[i] - u[i]);
-      if (lo && !hi) damp += u[i] - xl[i];
-      if (hi && !lo) damp += xu[i] - u[i];
-    }
+    for (int i = lanef(); i < nw; i += WAVE) barrier_ctrl1(i, u[i], logs, damp);
+  }
+  // one control's barrier terms at the value ui (a register: the trial point's controls
+  // are formed and consumed in the same pass, no store -> load round trip)
+  __device__ __forceinline__ void barrier_ctrl1(int i, double ui, double& logs, double& damp) const {
+    const bool lo = hasl(xl[i]), hi = hasu(xu[i]);
+    if (lo) logs += log(ui - xl[i]);
+    if (hi) logs += log(xu[i] - ui);
+    if (lo && !hi) damp += ui - xl[i];
+    if (hi && !lo) damp += xu[i] - ui;
   }
   __device__ __forceinline__ void barrier_row(int r, bool on, double sv, double& logs, double& damp) const {
     const double lo_ = dl[r], hi_ = du[r];
@@ -1868,15 +1875,21 @@ struct Solver {
   __device__ __forceinline__ bool trial_resto(double a, const GLB double* dUs, const RV* dss,
                                               const GLB double* dps, const GLB double* dns, double& fo,
                                               double& phit, double& tht) {
-    for (int i = lanef(); i < nw; i += WAVE) Ut[i] = U[i] + a * dUs[i];
-    sync();
-    rollout(Ut, Xt);
-    fo = df * eval_fg(Xt, dt, dc);
-    // theta_R, the barrier sums and the p/n sums in one pass over the rows (each
+    // the trial controls, their barrier terms and the proximity term in one pass (each
     // accumulator keeps the per-lane order of barrier_obj / resto_pn_terms)
     double th = 0.0, logs = 0.0, damp = 0.0, pn = 0.0, lg = 0.0, prox = 0.0;
+    for (int i = lanef(); i < nw; i += WAVE) {
+      const double ui = U[i] + a * dUs[i];
+      Ut[i] = ui;
+      barrier_ctrl1(i, ui, logs, damp);
+      const double dd = ui - UR[i];
+      prox += dr2(i) * dd * dd;
+    }
+    sync();
+    rollout(U, Xt, dUs, a);
+    fo = df * eval_fg(Xt, dt, dc);
+    // theta_R, the barrier sums and the p/n sums in one pass over the rows
     bool bad = false;
-    barrier_ctrl(Ut, logs, damp);
     rows([&](int r, bool on) {
       const double sv = s[r] + a * dss[r], pv = pR[r] + a * dps[r], nv = nR[r] + a * dns[r];
       const double dtr = dt[r];
@@ -1889,10 +1902,6 @@ struct Solver {
         lg += l2;
       }
     });
-    for (int i = lanef(); i < nw; i += WAVE) {
-      const double dd = Ut[i] - UR[i];
-      prox += dr2(i) * dd * dd;
-    }
     tht = wsum(th);
     if (wany(bad)) return false;
     const double phb = barrier_fin(0.0, logs, damp);
@@ -2072,14 +2081,18 @@ struct Solver {
   // returns false on an evaluation error (NaN/Inf)
   __device__ __forceinline__ bool trial(double a, const GLB double* dUs, const RV* dss, double& ft, double& phit,
                         double& tht) {
-    for (int i = lanef(); i < nw; i += WAVE) Ut[i] = U[i] + a * dUs[i];
+    // the trial controls and their barrier terms in one pass
+    double th = 0.0, logs = 0.0, damp = 0.0;
+    for (int i = lanef(); i < nw; i += WAVE) {
+      const double ui = U[i] + a * dUs[i];
+      Ut[i] = ui;
+      barrier_ctrl1(i, ui, logs, damp);
+    }
     sync();
-    rollout(Ut, Xt);
+    rollout(U, Xt, dUs, a);
     ft = df * eval_fg(Xt, dt, dc);
     // theta and the barrier sums in one pass over the rows
-    double th = 0.0, logs = 0.0, damp = 0.0;
     bool bad = false;
-    barrier_ctrl(Ut, logs, damp);
     rows([&](int r, bool on) {
       const double sv = s[r] + a * dss[r], dtr = dt[r];
       barrier_row(r, on, sv, logs, damp);
