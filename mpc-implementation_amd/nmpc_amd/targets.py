@@ -29,6 +29,12 @@ SCHEDULES = {
     ],
     # Python/Race Track 2.py:28-36
     "race_track_2": [(0, 12.0, 0.0), (500, 12.0, PI / 100), (1000, 12.0, 0.0), (1500, 12.0, PI / 100)],
+    # MATLAB/Dynamic Obstacles/shift1.m:9 (con_t = [15; 0.12] every step): the no-gimbal
+    # NMPC_TT.m run and, by the reading in tests/golden/gen_reference_runs.py, the
+    # Dynamic Obstacle avoidance.m run (whose shift1 call at :251 passes sc where
+    # shift1.m expects the target)
+    "matlab_nmpc_tt": [(0, 15.0, 0.12)],
+    "dynamic_obstacles": [(0, 15.0, 0.12)],
     # Python/T_Trajectory.py:25-57
     "t_trajectory": [
         (0, 13.5, 0.0), (100, 13.5, (PI / 2) / 12), (160, 13.5, 0.0), (260, 13.5, -(PI / 2) / 12),

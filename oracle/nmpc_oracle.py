@@ -566,11 +566,48 @@ def _compare_le(lhs, rhs, basval):
     return lhs - rhs <= 10.0 * EPS * abs(basval)
 
 
+class _Chol:
+    """Cholesky factor of the condensed Newton matrix and its solve.  variant 0 is the
+    plain factorisation (the committed fixtures); variant v > 0 factors P M P^T for a fixed
+    symmetric permutation P of the variables (IpoptDense.la_variant): 1 reverses the
+    order, 2 takes the even then the odd positions, 3 rotates by a third.  Each is the
+    same Newton step in exact arithmetic and differs from variant 0 by rounding alone."""
+
+    def __init__(self, M, variant=0):
+        n = M.shape[0]
+        self.perm = None
+        if variant == 1:
+            self.perm = np.arange(n)[::-1]
+        elif variant == 2:
+            self.perm = np.concatenate([np.arange(0, n, 2), np.arange(1, n, 2)])
+        elif variant == 3:
+            self.perm = np.roll(np.arange(n), n // 3)
+        self.L = np.linalg.cholesky(M if self.perm is None else M[np.ix_(self.perm, self.perm)])
+
+    def solve(self, b):
+        if self.perm is not None:
+            b = b[self.perm]
+        t = np.linalg.solve(self.L, b)
+        x = np.linalg.solve(self.L.T, t)
+        if self.perm is None:
+            return x
+        out = np.empty_like(x)
+        out[self.perm] = x
+        return out
+
+
 class IpoptDense:
     """Dense restatement of IPOPT on the reference single-shooting NLP."""
 
-    def __init__(self, prob: Problem, opts=None):
+    def __init__(self, prob: Problem, opts=None, la_variant=0):
+        """la_variant (parity diagnostics only): 0 = the fixtures' linear algebra; 1..3 = the
+        same Cholesky factorisation and solves with the variables symmetrically permuted
+        (P M P^T, _Chol) -- mathematically the identical Newton step, different by
+        rounding alone.  Running a step under both measures how far that
+        step's result moves under rounding-level changes of the linear algebra
+        (tests/golden/gen_rounding_spread.py)."""
         self.prob = prob
+        self.la_variant = int(la_variant)
         o = dict(IPOPT_DEFAULTS)
         if opts:
             for k, v in opts.items():
@@ -761,6 +798,7 @@ class IpoptDense:
         last_obj, curr_obj, last_obj_iter = -1e50, -1e50, -1
         it = 0
         tr = []
+        self.chk = []
         status = None
         acc_point = None
         # watchdog procedure (BacktrackingLineSearch): successive shortened steps,
@@ -987,7 +1025,7 @@ class IpoptDense:
                     # without 1/D so rows with no bound (D = 0) stay finite
                     M = Wr + np.diag(SigX + delta_) + JR.T @ (Dt[:, None] * JR)
                     try:
-                        fact = np.linalg.cholesky(sq(M))
+                        fact = _Chol(sq(M), self.la_variant)
                         break
                     except np.linalg.LinAlgError:
                         if delta_ == 0.0:
@@ -1016,7 +1054,7 @@ class IpoptDense:
                     Dr = Dt * (c_ + rp / Spd - rn / Snd) + rs_ * den
                     rhs = -(gphi + JR.T @ (yR + Dr))
                     dx_ = np.zeros(n)
-                    dx_[F] = np.linalg.solve(fact.T, np.linalg.solve(fact, rhs[F]))
+                    dx_[F] = fact.solve(rhs[F])
                     jd = JR @ dx_
                     dy_ = Dt * jd + Dr
                     dp_ = (dy_ - rp) / Spd
@@ -1211,6 +1249,9 @@ class IpoptDense:
                 status = INVALID_NUMBER_DETECTED
                 break
             u_dinf, u_cviol, u_cmp = dinf / df, cviol_unscaled(d, dc, gl_, gu_, slm, sum_, eq, lbg), cmp / df
+            if trace:  # the convergence check's quantities (parity diagnostics: which test decided)
+                sd_, sc_ = err_scaling(y, zl, zu, vl, vu)
+                self.chk.append(dict(it=it, err=err, dinf=dinf / sd_, cviol=cviol, cmp=cmp / sc_, f=f))
             if (err <= o["tol"] and u_dinf <= o["dual_inf_tol"] and u_cviol <= o["constr_viol_tol"]
                     and u_cmp <= o["compl_inf_tol"]):
                 status = SOLVE_SUCCEEDED
@@ -1284,7 +1325,7 @@ class IpoptDense:
                         if fact is None:
                             raise np.linalg.LinAlgError("wrong inertia of the augmented system")
                     else:
-                        fact = np.linalg.cholesky(sq(M))
+                        fact = _Chol(sq(M), self.la_variant)
                     break
                 except np.linalg.LinAlgError:
                     if delta == 0.0:
@@ -1313,8 +1354,7 @@ class IpoptDense:
                     sol = np.linalg.solve(fact, np.concatenate([rhs[F], -rd_[eq]]))
                     dx_[F], dyc = sol[:nf], sol[nf:]
                 else:
-                    t = np.linalg.solve(fact, rhs[F])
-                    dx_[F] = np.linalg.solve(fact.T, t)
+                    dx_[F] = fact.solve(rhs[F])
                 ds_ = np.where(eq, 0.0, J @ dx_ + rd_)
                 dy_ = D * ds_ + rs
                 if neq:

@@ -29,7 +29,7 @@ for rep in range(2):
 ms = e0.elapsed_time(e1)
 it = out["iters"].cpu().numpy()
 tr = s.read_trace(B)
-tot = tr[:, s.max_iter:, :].reshape(B, 24)[:, 15]
+tot = tr[:, s.max_iter:, :].reshape(B, -1)[:, :24][:, 15]
 print(f"class={os.environ.get('NMPC_FORCE_CLASS', 'A')} lds_pad={os.environ.get('NMPC_LDS_BYTES', '-')} "
       f"B={B} kernel_info={s.kernel_info()} kernel {ms:.2f} ms; iters mean {it.mean():.2f} max {it.max()}; "
       f"cycles/iter per scenario mean {np.mean(tot / np.maximum(it, 1)):.4e}; "

@@ -1,0 +1,147 @@
+"""Rounding spread of the oracle on the reference runs (test infrastructure only).
+
+The reference-run fixtures (gen_reference_runs.py -> ref_run_<name>.npz) are one
+solver's answer: the numpy IPOPT restatement with one particular order of floating-point
+operations.  How much of that answer is fixed by the algorithm, and how much by rounding,
+is measured here by re-solving with solvers that run the SAME algorithm and differ from
+the fixture's solver by rounding alone:
+
+  numpy1..3  the numpy oracle with la_variant 1..3 (oracle/nmpc_oracle.py _Chol: the
+             identical Newton step from the Cholesky factor of P M P^T for a fixed
+             permutation P of the variables);
+  cpp        the compiled restatement (oracle/cpu_ipopt.cpp: the same control flow with
+             the Riccati recursion for the Newton step).
+
+Two measurements per run, written to ref_run_<name>_spread.npz:
+
+  per step  (numpy1..3) each step's (w, p) of the fixture solved again: status,
+            iterations, and the largest relative deviation of x and f from the fixture.
+            A step whose result moves under these rounding-level changes is a step at
+            which the fixture's own x / iteration count is not determined beyond rounding
+            (a termination test decided within rounding of its threshold, or a flat
+            optimum); tests/test_gpu_reference_runs.py asserts that every GPU-vs-fixture
+            difference of status or of a converged x at 1e-6 falls on such a step, and
+            that the GPU differs from the fixture no more often than these solvers do.
+  whole run (cpp, numpy1..3) the run's whole closed loop: the step at which it parts from
+            the fixture's loop (gen_reference_runs.agree_prefix, the test's definition),
+            its statuses / iterations per step and its printed result (FOV-error sum).
+            The loops are chaotic, so where two rounding-level variants part and how far
+            their whole-run sums spread is the yardstick the GPU's loop is held to.
+
+    python tests/golden/gen_rounding_spread.py [<run>|all] [--jobs 8]
+"""
+import argparse
+import multiprocessing as mp
+import os
+import sys
+import time
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, HERE)
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "mpc-implementation_amd"))
+
+import gen_reference_runs as grr  # noqa: E402
+
+VARIANTS = (1, 2, 3)
+WHOLE = ("cpp", "numpy1", "numpy2", "numpy3")
+CHUNK = 100
+
+
+def _fixture(name):
+    return dict(np.load(os.path.join(HERE, f"ref_run_{name}.npz")))
+
+
+def warm_starts(name, z):
+    """The warm start of every step of the fixture's loop (shift of the previous x)."""
+    c = grr.RUNS[name]
+    nu = grr.run_problem(name).nu
+    K = len(z["status"])
+    W = np.zeros((K, z["x"].shape[1]))
+    for k in range(1, K):
+        W[k] = grr.warm_start(z["x"][k - 1], c["N"], nu)
+    return W
+
+
+def per_step_job(args):
+    name, v, k0, k1 = args
+    from threadpoolctl import threadpool_limits
+    from oracle import nmpc_oracle as orc
+
+    threadpool_limits(1)
+    z = _fixture(name)
+    W = warm_starts(name, z)
+    ipo = orc.IpoptDense(grr.run_problem(name), orc.REFERENCE_OPTS, la_variant=v)
+    out = []
+    for k in range(k0, k1):
+        r = ipo.solve(W[k], z["lbx"], z["ubx"], z["lbg"], z["ubg"], z["p"][k])
+        dx = float(np.max(np.abs(r["x"] - z["x"][k]) / (1 + np.abs(z["x"][k]))))
+        df = float(abs(r["f"] - z["f"][k]) / (1 + abs(z["f"][k])))
+        out.append((k, int(r["status"]), int(r["iter"]), dx, df))
+    return name, v, out
+
+
+def whole_job(args):
+    name, solver = args
+    z = _fixture(name)
+    o = grr.run(name, solver, log_every=500)
+    nx, nu = grr.run_problem(name).nx, grr.run_problem(name).nu
+    part = grr.agree_prefix(z, o["p"][:, :nx], o["status"], o["x"][:, :nu], o["f"])
+    return name, solver, dict(part=part, fov_sum=float(o["fov_sum"]), status=o["status"].astype(np.int16),
+                              iter=o["iter"].astype(np.int16))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("run", nargs="?", default="all")
+    ap.add_argument("--jobs", type=int, default=8)
+    a = ap.parse_args()
+    names = list(grr.RUNS) if a.run == "all" else [a.run]
+    jobs_w = [(n, s) for n in names for s in WHOLE]
+    jobs_w.sort(key=lambda j: -grr.RUNS[j[0]]["K"] * (0.05 if j[1] == "cpp" else 1.0))
+    jobs_s = []
+    for n in names:
+        K = len(_fixture(n)["status"])
+        jobs_s += [(n, v, k0, min(K, k0 + CHUNK)) for v in VARIANTS for k0 in range(0, K, CHUNK)]
+    t0 = time.time()
+    res_s = {n: {v: [] for v in VARIANTS} for n in names}
+    res_w = {n: {} for n in names}
+    with mp.get_context("fork").Pool(a.jobs) as pool:
+        aw = pool.map_async(whole_job, jobs_w, chunksize=1)
+        for n, v, out in pool.imap_unordered(per_step_job, jobs_s):
+            res_s[n][v] += out
+        print(f"per-step spread done in {time.time() - t0:.0f}s", flush=True)
+        for n, s, r in aw.get():
+            res_w[n][s] = r
+    for n in names:
+        z = _fixture(n)
+        K = len(z["status"])
+        st = np.zeros((len(VARIANTS), K), np.int16)
+        it = np.zeros((len(VARIANTS), K), np.int16)
+        dx = np.zeros((len(VARIANTS), K))
+        df = np.zeros((len(VARIANTS), K))
+        for i, v in enumerate(VARIANTS):
+            for k, s_, n_, x_, f_ in res_s[n][v]:
+                st[i, k], it[i, k], dx[i, k], df[i, k] = s_, n_, x_, f_
+        out = dict(step_variants=np.array(VARIANTS), step_status=st, step_iter=it, step_dev_x=dx, step_dev_f=df,
+                   run_solvers=np.array(WHOLE), run_part=np.array([res_w[n][s]["part"] for s in WHOLE]),
+                   run_fov_sum=np.array([res_w[n][s]["fov_sum"] for s in WHOLE]),
+                   run_status=np.stack([res_w[n][s]["status"] for s in WHOLE]),
+                   run_iter=np.stack([res_w[n][s]["iter"] for s in WHOLE]),
+                   fixture_fov_sum=float(z["fov_sum"]))
+        np.savez_compressed(os.path.join(HERE, f"ref_run_{n}_spread.npz"), **out)
+        conv = np.isin(z["status"], (0, 1))
+        print(f"{n}: per step (vs fixture) " + "; ".join(
+            f"la{v}: status {int((st[i] != z['status']).sum())}, iter {int((it[i] != z['iter']).sum())}, "
+            f"conv x>1e-6 {int((conv & (st[i] == z['status']) & (dx[i] > 1e-6)).sum())}"
+            for i, v in enumerate(VARIANTS)), flush=True)
+        print(f"{n}: whole run parts at " + ", ".join(f"{s} {res_w[n][s]['part']}" for s in WHOLE)
+              + f"; FOV-error sums fixture {float(z['fov_sum']):.3f}, "
+              + ", ".join(f"{s} {res_w[n][s]['fov_sum']:.3f}" for s in WHOLE), flush=True)
+
+
+if __name__ == "__main__":
+    main()
