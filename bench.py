@@ -55,30 +55,35 @@ def survey_bytes_per_step(spec, ibar):
 def pmc_summary(kernel, steps, batch, warmup):
     """Counters of `kernel`'s timed launch from the newest committed rocprofv3 PMC
     summary (profiles/r*_pmc.csv, written by scripts/rocpd_summary.py from the passes
-    of scripts/profile_round.sh), used only when the profiled runs had this run's
-    steps, batch and warm-up.  HBM-side bytes = 2 x FETCH_SIZE + WRITE_SIZE (KB -> B):
+    of scripts/profile_round.sh) whose profiled runs had this run's kernel, steps, batch
+    and warm-up (config 3 and config 5 have their own files; the newest file that holds
+    matching rows for both byte counters is taken).  HBM-side bytes = 2 x FETCH_SIZE + WRITE_SIZE (KB -> B):
     FETCH_SIZE counts half the bytes of 8 B/lane and 16 B/lane reads alike on gfx950
     (scripts/fetch_calib.hip, profiles/r02_fetch_calib.csv: 1 GiB read -> 512 MiB
     counted for both widths; WRITE_SIZE exact for 8 B/lane stores).  Both count
     L2-to-fabric traffic, Infinity-Cache hits included (MI355X_MICROARCH.md, HBM)."""
     import csv
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc.csv")))
-    if not files:
-        return None
-    vals, run = {}, {}
-    for row in csv.DictReader(open(files[-1])):
-        if (kernel in row["kernel"] and row.get("steps", "") == str(steps) and row.get("batch", "") == str(batch)
-                and row.get("warmup", "") == str(warmup)):
-            # the launch pairs the problem's class with the equality class behind a device
-            # flag (nmpc_create); the one that ran is the row with the counts
-            if float(row["value"]) >= vals.get(row["counter"], -1.0):
-                vals[row["counter"]] = float(row["value"])
-                run[row["counter"]] = {k: row.get(k) for k in ("ibar", "kernel_ms", "bench_value")}
-    if "FETCH_SIZE" not in vals or "WRITE_SIZE" not in vals:
+    # newest round first; within a round any file (r04_pmc.csv, r04_cfg5_pmc.csv, ...)
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc.csv")),
+                   key=lambda f: (os.path.basename(f)[:3], f), reverse=True)
+    for path in files:
+        vals, run = {}, {}
+        with open(path) as fh:
+            for row in csv.DictReader(fh):
+                if (kernel in row["kernel"] and row.get("steps", "") == str(steps)
+                        and row.get("batch", "") == str(batch) and row.get("warmup", "") == str(warmup)):
+                    # the launch pairs the problem's class with the equality class behind a
+                    # device flag (nmpc_create); the one that ran is the row with the counts
+                    if float(row["value"]) >= vals.get(row["counter"], -1.0):
+                        vals[row["counter"]] = float(row["value"])
+                        run[row["counter"]] = {k: row.get(k) for k in ("ibar", "kernel_ms", "bench_value")}
+        if "FETCH_SIZE" in vals and "WRITE_SIZE" in vals:
+            break
+    else:
         return None
     out = {"traffic": (2.0 * vals["FETCH_SIZE"] + vals["WRITE_SIZE"]) * 1024.0,
-           "source": os.path.relpath(files[-1], ROOT), "profiled_runs": run}
+           "source": os.path.relpath(path, ROOT), "profiled_runs": run}
     if vals.get("SQ_WAVE_CYCLES"):
         wc = vals["SQ_WAVE_CYCLES"]
         out["sq"] = {"wait_any_frac": vals.get("SQ_WAIT_ANY", 0) / wc,
@@ -90,13 +95,15 @@ def pmc_summary(kernel, steps, batch, warmup):
     return out
 
 
-def cpu_baseline(spec_cfg, cfg, P, lbx, ubx, lbg, ubg, K, budget_s=15.0):
+def cpu_baseline(spec_cfg, cfg, P, lbx, ubx, lbg, ubg, K, W=0, p_step=None, budget_s=15.0):
     """Time the compiled CPU restatement (oracle/cpu_ipopt.cpp: C++/OpenMP, the same
     IPOPT restatement with a Riccati Newton step, pinned to the numpy oracle's
-    fixtures by tests/test_cpu_restatement.py) on the bench's own workload: the same
-    scenarios through the same warm-started closed loop (solve + shift, K steps per
-    scenario from w = 0), one scenario per OpenMP thread at a time, until the
-    budget runs out (scenarios split across cores)."""
+    fixtures by tests/test_cpu_restatement.py) on the bench's own workload and window:
+    the same scenarios advanced by the same W untimed warm-up MPC steps from w = 0,
+    then the same K timed warm-started closed-loop steps (solve + shift) from there --
+    the (scenario, step) window of the GPU's timed launch -- one scenario per OpenMP
+    thread at a time, until the budget runs out (scenarios split across
+    cores).  p_step (W + K, np): the moving obstacles' per-step displacement (config 5)."""
     sys.path.insert(0, ROOT)
     from oracle import cpu_ipopt, nmpc_oracle as orc
 
@@ -107,9 +114,17 @@ def cpu_baseline(spec_cfg, cfg, P, lbx, ubx, lbg, ubg, K, budget_s=15.0):
     nthr = max(1, min(16, ncpu))  # the GPU box's CPU share is 16
     layout = None if spec_cfg.n_obs == 0 else ("race_track_2" if spec_cfg.n_obs == 10 else "nmpc_tt")
     prob = orc.make_problem(layout, N=spec_cfg.N, T=spec_cfg.T, model=spec_cfg.model)
+    # the W warm-up steps, untimed, for every scenario (the GPU runs them as W per-step launches)
+    P1, W1 = P, None
+    if W > 0:
+        r0 = cpu_ipopt.closed_loop(prob, P, W, lbx, ubx, lbg, ubg, orc.REFERENCE_OPTS, vt=12.0, wt=0.01,
+                                   p_step=None if p_step is None else p_step[:W], threads=nthr)
+        P1, W1 = r0["p"], r0["w"]
+    cpu_baseline.start = (P1, W1)
     t0 = time.perf_counter()
-    r = cpu_ipopt.closed_loop(prob, P, K, lbx, ubx, lbg, ubg, orc.REFERENCE_OPTS, vt=12.0, wt=0.01,
-                              budget_s=budget_s, threads=nthr)
+    r = cpu_ipopt.closed_loop(prob, P1, K, lbx, ubx, lbg, ubg, orc.REFERENCE_OPTS, vt=12.0, wt=0.01,
+                              p_step=None if p_step is None else p_step[W:W + K], budget_s=budget_s,
+                              threads=nthr, W0=W1)
     wall = time.perf_counter() - t0
     done = r["steps"]
     n = int(done.sum())
@@ -121,10 +136,10 @@ def cpu_baseline(spec_cfg, cfg, P, lbx, ubx, lbg, ubg, K, budget_s=15.0):
     its = np.concatenate([r["iter"][b, :done[b]] for b in rows]) if len(rows) else np.zeros(0)
     sts = np.concatenate([r["status"][b, :done[b]] for b in rows]) if len(rows) else np.zeros(0, int)
     tsv = np.concatenate([r["solve_s"][b, :done[b]] for b in rows]) if len(rows) else np.zeros(0)
-    # cold-start leg (cold u = 0 and warm-started): every scenario's first
-    # NLP from u = 0, the same threads
+    # cold-start leg (cold u = 0 and warm-started): every scenario's NLP of
+    # the timed window's first step from u = 0, the same threads
     t1 = time.perf_counter()
-    rc = cpu_ipopt.solve_batch(prob, np.zeros((P.shape[0], spec_cfg.nw)), P, lbx, ubx, lbg, ubg,
+    rc = cpu_ipopt.solve_batch(prob, np.zeros((P.shape[0], spec_cfg.nw)), P1, lbx, ubx, lbg, ubg,
                                orc.REFERENCE_OPTS, threads=nthr)
     cwall = time.perf_counter() - t1
 
@@ -136,8 +151,9 @@ def cpu_baseline(spec_cfg, cfg, P, lbx, ubx, lbg, ubg, K, budget_s=15.0):
             "status_histogram": {int(k): int(v) for k, v in zip(*np.unique(rc["status"], return_counts=True))},
             "sample": f"cold solves (u = 0) of all {P.shape[0]} bench scenarios, {nthr} threads"}
     return {"value": n / wall, "unit": "MPC steps/s", "cores": nthr, "kind": "port",
-            "sample": f"{n} warm-started closed-loop MPC steps (solve + shift, up to {K} per scenario, "
-                      f"{len(rows)} of the bench's config-{cfg} scenarios) by oracle/cpu_ipopt.cpp (CPU "
+            "sample": f"{n} warm-started closed-loop MPC steps (solve + shift) of the GPU's timed window -- "
+                      f"steps {W}..{W + K - 1} after the same {W} untimed warm-up steps, up to {K} per scenario, "
+                      f"{len(rows)} of the bench's config-{cfg} scenarios -- by oracle/cpu_ipopt.cpp (CPU "
                       f"restatement, not CasADi: C++/OpenMP IPOPT restatement with a Riccati step), "
                       f"{nthr} threads, budget {budget_s:.0f}s, wall {wall:.1f}s",
             "mean_ip_iterations": float(its.mean()) if n else None,
@@ -147,11 +163,12 @@ def cpu_baseline(spec_cfg, cfg, P, lbx, ubx, lbg, ubg, K, budget_s=15.0):
             "cold_start": cold}
 
 
-def parity_sample(solver, spec, P, K, records, bnd, dev, tol=1e-6):
+def parity_sample(solver, spec, start, K, records, bnd, dev, p_step=None, tol=1e-6):
     """GPU vs the CPU leg on the same (scenario, step) pairs: the CPU leg's scenarios
-    rerun through nmpc_closed_loop_dev from the same start (w = 0, the same p and
-    target controls), compared step by step until a chain first disagrees -- status,
-    and for converged steps u0 and f within tol (1 + |ref|) (the north-star 1e-6)."""
+    rerun through nmpc_closed_loop_dev from the CPU leg's own start of the timed window
+    (its p and warm start after the W warm-up steps, the same target controls and
+    obstacle motion), compared step by step until a chain first disagrees -- status, and
+    for converged steps u0 and f within tol (1 + |ref|) (the north-star 1e-6)."""
     import torch
 
     rows = sorted({r[0] for r in records})
@@ -159,11 +176,14 @@ def parity_sample(solver, spec, P, K, records, bnd, dev, tol=1e-6):
         return None
     idx = {r: j for j, r in enumerate(rows)}
     B = len(rows)
+    P1, W1 = start
     f64 = dict(dtype=torch.float64, device=dev)
     hist = {"u": torch.empty(K, B, 6, **f64), "f": torch.empty(K, B, **f64),
             "status": torch.empty(K, B, dtype=torch.int32, device=dev)}
-    solver.closed_loop_device(K, *bnd, torch.tensor(P[rows], **f64).contiguous(), torch.zeros(B, spec.nw, **f64),
-                              torch.full((B,), 12.0, **f64), torch.full((B,), 0.01, **f64), hist)
+    w0 = torch.zeros(B, spec.nw, **f64) if W1 is None else torch.tensor(W1[rows], **f64).contiguous()
+    solver.closed_loop_device(K, *bnd, torch.tensor(P1[rows], **f64).contiguous(), w0,
+                              torch.full((B,), 12.0, **f64), torch.full((B,), 0.01, **f64), hist,
+                              p_step=None if p_step is None else torch.tensor(p_step, **f64).contiguous())
     H = {k: v.cpu().numpy() for k, v in hist.items()}
     by = {}
     for row, k, st, u0, f in records:
@@ -230,10 +250,14 @@ def main():
     spec = config_spec(args.config)
     B, K, W = args.batch, args.steps, args.warmup
     cpu_res = None
+    ps_np = None
+    if spec.np > spec.np_min:  # moving obstacles (config 5), see pstep below
+        from nmpc_amd.targets import obstacle_steps
+        ps_np = obstacle_steps(195, W + K, spec.np)
     if world == 1 and not args.no_cpu_baseline:  # OpenMP threads, before the GPU is initialised
         lb = spec.bounds()
-        cpu_res = cpu_baseline(spec, args.config, draw_scenarios(spec, B, seed=1000 + args.config), *lb, K,
-                               budget_s=args.cpu_budget)
+        cpu_res = cpu_baseline(spec, args.config, draw_scenarios(spec, B, seed=1000 + args.config), *lb, K, W,
+                               p_step=ps_np, budget_s=args.cpu_budget)
     # NMPC_BENCH_BACKEND=gloo rehearses the multi-rank path on one GPU (all ranks on
     # cuda:0); the measured configuration is one process per GPU over RCCL ("nccl")
     backend = os.environ.get("NMPC_BENCH_BACKEND", "nccl")
@@ -269,10 +293,7 @@ def main():
     stream = torch.cuda.current_stream()
     # moving obstacles (config 5: MATLAB/Dynamic Obstacles/Dynamic Obstacle avoidance.m:213-230,
     # from MPC iteration 195 as in the config-5 fixtures; the W warm-up steps come first)
-    pstep = None
-    if spec.np > spec.np_min:
-        from nmpc_amd.targets import obstacle_steps
-        pstep = torch.tensor(obstacle_steps(195, W + K, spec.np), **f64)
+    pstep = None if ps_np is None else torch.tensor(ps_np, **f64)
 
     def hist_bufs(k):
         return {"u": torch.empty(k, B, 6, **f64), "f": torch.empty(k, B, **f64), "fov": torch.zeros(k, B, **f64),
@@ -453,8 +474,8 @@ def main():
         if cpu_res is not None:
             res["cpu_baseline"] = cpu_res
             if world == 1 and getattr(cpu_baseline, "records", None):
-                res["parity_sample"] = parity_sample(solver, spec, P_all[:cpu_baseline.sample_rows], K,
-                                                     cpu_baseline.records, bnd, dev)
+                res["parity_sample"] = parity_sample(solver, spec, cpu_baseline.start, K, cpu_baseline.records,
+                                                     bnd, dev, p_step=None if ps_np is None else ps_np[W:W + K])
         print(json.dumps(res))
         if args.dump_rows and args.mode == "fused":
             np.save(args.dump_rows, fused.rows.cpu().numpy())

@@ -81,7 +81,8 @@ struct Lay {
   // restoration phase: reference/backup iterate, p/n and their multipliers, steps, filter
   int UR, zl0, zu0, s0, vl0, vu0, pR, nR, zpR, znR, dpR, dnR, dyR, dp2R, dn2R, dy2R, cms, filtR;
   int accU, accZl, accZu, accY;  // last acceptable iterate (BacktrackingLineSearch::StoreAcceptablePoint)
-  int eqi, eqS, eqy, eqy2;        // equality rows: indices, Schur factor, dy_c (row-indexed) of the step / SOC
+  int eqi, eqS, eqy, eqy2, weqy;  // equality rows: indices, Schur factor, dy_c (row-indexed) of the step / SOC,
+                                  // and the watchdog's stored dy_c
   // watchdog procedure: the stored iterate and its step (main loop; the restoration phase
   // reuses them, and adds its p, n, their multipliers and steps)
   int wU, wzl, wzu, wdU, ws, wy, wvl, wvu, wds, wpR, wnR, wzpR, wznR, wdpR, wdnR, wdyR;
@@ -135,7 +136,7 @@ constexpr Lay make_layout(int N, int m, bool lr, bool refine, bool eq) {
   L.wznR = g; g += al8(ng); L.wdpR = g; g += al8(ng); L.wdnR = g; g += al8(ng); L.wdyR = g; g += al8(ng);
   if (eq) {  // equality rows (the equality class only)
     L.eqi = g; g += al8(NMPC_MEQ / 2 + 1); L.eqS = g; g += al8(NMPC_MEQ * NMPC_MEQ + NMPC_MEQ);
-    L.eqy = g; g += al8(ng); L.eqy2 = g; g += al8(ng);
+    L.eqy = g; g += al8(ng); L.eqy2 = g; g += al8(ng); L.weqy = g; g += al8(ng);
   }
   if (!lr) { L.kf = g; g += al8(6 * N); }
   L.wstotal = g;
@@ -845,6 +846,7 @@ struct Solver {
   __device__ __forceinline__ GLB double* eqS_() const { return eqw(CAP::L.eqS); }
   __device__ __forceinline__ GLB double* eqy_() const { return eqw(CAP::L.eqy); }
   __device__ __forceinline__ GLB double* eqy2_() const { return eqw(CAP::L.eqy2); }
+  __device__ __forceinline__ GLB double* weqy_() const { return eqw(CAP::L.weqy); }
   // J_r dX (scaled row Jacobian times the state step at the row's stage), as in row_step
   __device__ __forceinline__ double row_jd(int r, const LDS double* dXs) const {
     const int k = r / m, i = r - k * m;
@@ -3221,6 +3223,10 @@ __device__ __forceinline__ int solve_one(Solver<CAP>& S, const Params* __restric
       for (int r = S.lanef(); r < ng; r += WAVE) {
         S.s[r] = S.wsl[r]; S.y[r] = S.wy[r]; S.vl[r] = S.wvl[r]; S.vu[r] = S.wvu[r]; S.ds[r] = S.wds[r];
       }
+      if constexpr (CAP::eq) {  // the stored step's equality-multiplier step (WdPoint's dy)
+        if (S.meq > 0)
+          for (int r = S.lanef(); r < ng; r += WAVE) S.eqy_()[r] = S.weqy_()[r];
+      }
       sync();
       S.rollout(S.U, S.X);
       f = S.df * S.eval_fg(S.X, S.d, S.dc);
@@ -3244,6 +3250,10 @@ __device__ __forceinline__ int solve_one(Solver<CAP>& S, const Params* __restric
       }
       for (int r = S.lanef(); r < ng; r += WAVE) {
         S.wsl[r] = S.s[r]; S.wy[r] = S.y[r]; S.wvl[r] = S.vl[r]; S.wvu[r] = S.vu[r]; S.wds[r] = S.ds[r];
+      }
+      if constexpr (CAP::eq) {
+        if (S.meq > 0)
+          for (int r = S.lanef(); r < ng; r += WAVE) S.weqy_()[r] = S.eqy_()[r];
       }
       const double at = S.frac_to_bound(tau, S.dU, S.ds);
       WD[0] = theta_ref; WD[1] = phi_ref; WD[2] = gbd; WD[3] = at; WD[4] = mu; WD[5] = S.delta;
@@ -4109,7 +4119,7 @@ struct nmpc_handle {
   LoopFn loop = nullptr;
   SchedFn sched = nullptr;
   // the equality class, launched paired with the class above behind a device flag
-  // (fp64 handles; null for the fp32 leg and when NMPC_FORCE_CLASS picks a class)
+  // (fp64 handles; null for the fp32 leg and when NMPC_FORCE_CLASS=E picks it as the class)
   KernFn kernE = nullptr;
   LoopFn loopE = nullptr;
   SchedFn schedE = nullptr;
@@ -4139,8 +4149,10 @@ struct nmpc_handle {
 
 
 
+// returns true when NMPC_FORCE_CLASS picked the equality class itself (which then needs
+// no partner); any other class, forced or not, is paired with the equality class
 static bool pick_class(const Params& P, KernFn* fn, LoopFn* lfn, SchedFn* sfn, int* lds_doubles, int* ws_doubles) {
-  bool forced = false;
+  bool forcedE = false;
   ClassFns c;
   const bool fit_a = P.N <= CapA::nmax && P.m <= CapA::mmax;
   if (P.o.linear_solver_fp32) c = fit_a ? nmpc_class_fns_A32() : nmpc_class_fns_C32();
@@ -4153,11 +4165,10 @@ static bool pick_class(const Params& P, KernFn* fn, LoopFn* lfn, SchedFn* sfn, i
     if (e[0] == 'B' && P.N <= CapB::nmax && P.m <= CapB::mmax && !P.o.linear_solver_fp32) c = nmpc_class_fns_B();
     if (e[0] == 'C' && !P.o.linear_solver_fp32) c = nmpc_class_fns_C();
     if (e[0] == 'D' && P.N <= CapD::nmax && P.m <= CapD::mmax && !P.o.linear_solver_fp32) c = nmpc_class_fns_D();
-    if (e[0] == 'E' && !P.o.linear_solver_fp32) c = nmpc_class_fns_E();
-    forced = e[0] != 0;
+    if (e[0] == 'E' && !P.o.linear_solver_fp32) { c = nmpc_class_fns_E(); forcedE = true; }
   }
   *fn = c.fn; *lfn = c.lfn; *sfn = c.sfn; *lds_doubles = c.lds_doubles; *ws_doubles = c.ws_doubles;
-  return forced;
+  return forcedE;
 }
 
 // zero the gate flag and scan the batch's row bounds (stream-ordered before the pair)
@@ -4269,9 +4280,9 @@ int nmpc_create(const nmpc_desc* desc, nmpc_handle** out) {
   P.o = desc->opts;
   {
     int ldsd = 0;
-    const bool forced = pick_class(P, &h->kern, &h->loop, &h->sched, &ldsd, &h->ws_doubles);
+    const bool forcedE = pick_class(P, &h->kern, &h->loop, &h->sched, &ldsd, &h->ws_doubles);
     h->lds_bytes = ldsd * 8;
-    if (!P.o.linear_solver_fp32 && !forced) {
+    if (!P.o.linear_solver_fp32 && !forcedE) {
       const ClassFns ce = nmpc_class_fns_E();
       h->kernE = ce.fn; h->loopE = ce.lfn; h->schedE = ce.sfn; h->lds_bytesE = ce.lds_doubles * 8;
       if (ce.ws_doubles > h->ws_doubles) h->ws_doubles = ce.ws_doubles;
@@ -4633,10 +4644,18 @@ int nmpc_closed_loop_dev(nmpc_handle* h, int32_t B, int32_t K, const double* lbx
     }
     hipLaunchKernelGGL(h->sched, dim3(waves), dim3(WAVE), h->lds_bytes, (hipStream_t)stream,
                        (const Params*)h->dprm, (int)B, io, lp, q);
-    // the equality class on the same queues (exactly one of the pair runs)
-    if (h->schedE && h->residentE >= NXCD)
+    // the equality class on the same queues (exactly one of the pair runs); when its own
+    // occupancy cannot put a wave on every XCD, one workgroup per scenario instead, on the
+    // same completion-guard state (zeroed by nmpc_sched_init_kernel)
+    if (h->schedE && h->residentE >= NXCD) {
       hipLaunchKernelGGL(h->schedE, dim3(h->residentE < waves ? h->residentE : waves), dim3(WAVE), h->lds_bytesE,
                          (hipStream_t)stream, (const Params*)h->dprm, (int)B, io, lp, q);
+    } else if (h->loopE) {
+      Loop lpE = lp;
+      lpE.done = q.done;
+      hipLaunchKernelGGL(h->loopE, dim3(B), dim3(WAVE), h->lds_bytesE, (hipStream_t)stream,
+                         (const Params*)h->dprm, (int)B, io, lpE);
+    }
     h->last_policy = 1;
     h->last_waves = waves;
   } else {

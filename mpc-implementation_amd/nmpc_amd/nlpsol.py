@@ -253,7 +253,9 @@ class Solver:
         ``p_step`` (K,np), optional: added to p[11:] after each step (moving
         obstacles, targets.obstacle_steps).
         ``order`` (B,) int32 device tensor, optional: dispatch order, a permutation
-        of range(B) (schedule.longest_first); results do not depend on it.
+        of range(B) (schedule.longest_first); results do not depend on it.  Validated
+        (ValueError) when ``check`` is set; with ``check=False`` a non-permutation is
+        reported by check_closed_loop instead.
         ``check`` (default): synchronise and raise unless every scenario completed its K
         steps (check_closed_loop); pass False to stay asynchronous and call
         check_closed_loop later.
@@ -306,8 +308,11 @@ class Solver:
             assert order.dtype == torch.int32 and order.is_cuda and order.is_contiguous()
             assert tuple(order.shape) == (B,), tuple(order.shape)
             # a dispatch order must be a permutation: a duplicate would run one scenario
-            # on two waves at once (the completion check would still flag the missing one)
-            if _validate_order and not torch.equal(torch.sort(order).values,
+            # on two waves at once (the completion check would still flag the missing one).
+            # Checked on the synchronous path only: the check reads the device tensor back,
+            # and check=False promises no host synchronisation (the device completion guard
+            # reports a scenario a bad order leaves unrun)
+            if check and _validate_order and not torch.equal(torch.sort(order).values,
                                                    torch.arange(B, dtype=torch.int32, device=order.device)):
                 raise ValueError("order must be a permutation of range(B)")
         if stream is None:

@@ -2297,10 +2297,15 @@ int nmpc_cpu_solve_batch(const nmpc_cpu_problem* prob, const double* opts, int64
 // once budget_s seconds have passed (budget_s <= 0: no limit); steps_done[b] says
 // how many steps scenario b ran.  Histories: status / iter (B x K), u0 (B x K x nu), f,
 // and (nullable) each solve's wall time in seconds (B x K).
+// w0 (nullable: zeros) is each scenario's warm start for its first step; p_out / w_out
+// (nullable) receive the state after its last step (the next step's p and warm start), so a
+// loop can be continued from where another one stopped (bench.py: W untimed warm-up steps,
+// then the K timed ones from the same state as the GPU's timed launch)
 int nmpc_cpu_closed_loop(const nmpc_cpu_problem* prob, const double* opts, int64_t B, int32_t K, const double* p0,
-                         const double* lbx, const double* ubx, const double* lbg, const double* ubg, double vt,
-                         double wt, const double* p_step, double budget_s, int nthreads, int32_t* status_out, int32_t* iter_out,
-                         double* u0_out, double* f_out, int32_t* steps_done, double* solve_s) {
+                         const double* w0, const double* lbx, const double* ubx, const double* lbg, const double* ubg,
+                         double vt, double wt, const double* p_step, double budget_s, int nthreads, int32_t* status_out,
+                         int32_t* iter_out, double* u0_out, double* f_out, int32_t* steps_done, double* solve_s,
+                         double* p_out, double* w_out) {
   if (!prob || !opts || B < 0 || K < 0) return 1;
   const Prob P = make_prob(*prob);
   const Opts o = opts_from(opts);
@@ -2315,7 +2320,8 @@ int nmpc_cpu_closed_loop(const nmpc_cpu_problem* prob, const double* opts, int64
 #pragma omp for schedule(dynamic, 1)
     for (int64_t b = 0; b < B; ++b) {
       std::memcpy(p.data(), p0 + b * P.np, sizeof(double) * P.np);
-      std::fill(w.begin(), w.end(), 0.0);
+      if (w0) std::memcpy(w.data(), w0 + b * P.n, sizeof(double) * P.n);
+      else std::fill(w.begin(), w.end(), 0.0);
       int k = 0;
       for (; k < K; ++k) {
         if (budget_s > 0 && elapsed() >= budget_s) break;
@@ -2332,6 +2338,8 @@ int nmpc_cpu_closed_loop(const nmpc_cpu_problem* prob, const double* opts, int64
           for (int j = P.nx + 3; j < P.np; ++j) p[j] = p[j] + p_step[(int64_t)k * P.np + j];
       }
       steps_done[b] = k;
+      if (p_out) std::memcpy(p_out + b * P.np, p.data(), sizeof(double) * P.np);
+      if (w_out) std::memcpy(w_out + b * P.n, w.data(), sizeof(double) * P.n);
     }
   }
   return 0;

@@ -45,8 +45,9 @@ def lib():
         dp, ip = C.POINTER(C.c_double), C.POINTER(C.c_int32)
         L.nmpc_cpu_solve_batch.argtypes = [C.POINTER(CpuProblem), dp, C.c_int64, dp, dp, dp, dp, dp, dp,
                                            dp, dp, dp, dp, dp, ip, ip, C.c_int, dp]
-        L.nmpc_cpu_closed_loop.argtypes = [C.POINTER(CpuProblem), dp, C.c_int64, C.c_int32, dp, dp, dp, dp, dp,
-                                           C.c_double, C.c_double, dp, C.c_double, C.c_int, ip, ip, dp, dp, ip, dp]
+        L.nmpc_cpu_closed_loop.argtypes = [C.POINTER(CpuProblem), dp, C.c_int64, C.c_int32, dp, dp, dp, dp, dp, dp,
+                                           C.c_double, C.c_double, dp, C.c_double, C.c_int, ip, ip, dp, dp, ip, dp,
+                                           dp, dp]
         _lib = L
     return _lib
 
@@ -114,24 +115,28 @@ def solve_batch(prob, W0, P, lbx, ubx, lbg, ubg, opts=None, threads=0):
 
 
 def closed_loop(prob, P0, K, lbx, ubx, lbg, ubg, opts=None, vt=12.0, wt=0.01, p_step=None, budget_s=0.0,
-                threads=0):
+                threads=0, W0=None):
     """K warm-started MPC steps per scenario (solve + shift_timestep; obstacle
-    parameters advanced by p_step[k] (K, np) after step k), from p0 rows and w = 0.
-    Stops starting new steps after budget_s seconds (0: no limit).  Returns status /
-    iter (B, K), u0 (B, K, nu), f (B, K), steps (B,), and solve_s (B, K): each solve's
-    wall time in seconds."""
+    parameters advanced by p_step[k] (K, np) after step k), from p0 rows and the warm
+    starts W0 (B, nw; None: w = 0).  Stops starting new steps after budget_s seconds (0:
+    no limit).  Returns status / iter (B, K), u0 (B, K, nu), f (B, K), steps (B,),
+    solve_s (B, K): each solve's wall time in seconds, and p / w (B, np) / (B, nw): the
+    state after each scenario's last step, from which the loop continues."""
     P0 = _f64(P0)
     ps = None if p_step is None else _f64(p_step, (K, prob.np_))
     B = P0.shape[0]
+    w0 = None if W0 is None else _f64(W0, (B, prob.nw))
     out = {"status": np.full((B, K), -1000, np.int32), "iter": np.zeros((B, K), np.int32),
            "u0": np.full((B, K, prob.nu), np.nan), "f": np.full((B, K), np.nan), "steps": np.zeros(B, np.int32),
-           "solve_s": np.full((B, K), np.nan)}
+           "solve_s": np.full((B, K), np.nan), "p": np.empty((B, prob.np_)), "w": np.empty((B, prob.nw))}
     cp = problem_struct(prob)
     oa = options_array(opts)
     bl = [_f64(b) for b in (lbx, ubx, lbg, ubg)]
-    rc = lib().nmpc_cpu_closed_loop(C.byref(cp), _p(oa), B, int(K), _p(P0), *[_p(b) for b in bl], float(vt),
-                                    float(wt), None if ps is None else _p(ps), float(budget_s), int(threads), _i(out["status"]), _i(out["iter"]),
-                                    _p(out["u0"]), _p(out["f"]), _i(out["steps"]), _p(out["solve_s"]))
+    rc = lib().nmpc_cpu_closed_loop(C.byref(cp), _p(oa), B, int(K), _p(P0), None if w0 is None else _p(w0),
+                                    *[_p(b) for b in bl], float(vt), float(wt), None if ps is None else _p(ps),
+                                    float(budget_s), int(threads), _i(out["status"]), _i(out["iter"]),
+                                    _p(out["u0"]), _p(out["f"]), _i(out["steps"]), _p(out["solve_s"]),
+                                    _p(out["p"]), _p(out["w"]))
     if rc != 0:
         raise RuntimeError(f"nmpc_cpu_closed_loop failed ({rc})")
     return out

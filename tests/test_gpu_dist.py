@@ -113,3 +113,57 @@ def test_config4_eight_rank_bench_rehearsal_equals_single_rank():
     a, b = np.load(multi), np.load(single)
     assert a.shape == b.shape == (32768, 8 * 2)
     np.testing.assert_array_equal(a, b)
+
+
+def _rccl_rank(port, q):
+    """World size 1 over RCCL (backend "nccl") on cuda:0, the process group created before
+    any other GPU call of this process: gather_rows / gather_closed_loop take their
+    all_gather_into_tensor branch; a gloo group of the same rank gives the reference."""
+    import sys
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "mpc-implementation_amd"))
+    import torch
+    import torch.distributed as dist
+    from nmpc_amd import config_spec, draw_scenarios
+    from nmpc_amd.dist import gather_rows, gather_closed_loop, pack_result
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    gloo = dist.new_group(backend="gloo")
+    assert dist.get_backend() == "nccl" and dist.get_backend(gloo) == "gloo"
+    P = draw_scenarios(config_spec(3), TOTAL, seed=1003)
+    hist = _closed_loop(P, K)
+    torch.cuda.synchronize()
+    out = {}
+    for name, g in (("nccl", None), ("gloo", gloo)):
+        rows = gather_closed_loop(hist, 1, group=g, total=TOTAL)
+        res = gather_rows(pack_result(hist["u"][-1].contiguous(), hist["f"][-1], hist["status"][-1]), 1, group=g,
+                          total=TOTAL)
+        torch.cuda.synchronize()
+        out[name] = (rows.cpu().numpy(), res.cpu().numpy(), rows.device.type)
+    q.put(out)
+    dist.destroy_process_group(gloo)
+    dist.destroy_process_group()
+
+
+def test_rccl_world_size_one_gather_equals_gloo():
+    """The RCCL branch of nmpc_amd.dist (all_gather_into_tensor on device tensors, the
+    path bench.py takes on a multi-GPU node) runs on this one-GPU box at world size 1 and
+    gives bitwise the rows of the gloo branch (host-staged all_gather) and of the local
+    packing."""
+    import torch.multiprocessing as mp
+    from nmpc_amd.dist import pack_closed_loop
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    proc = ctx.Process(target=_rccl_rank, args=(_free_port(), q))
+    proc.start()
+    out = q.get(timeout=240)
+    proc.join(timeout=60)
+    assert proc.exitcode == 0
+    (rn, sn, dev_n), (rg, sg, _) = out["nccl"], out["gloo"]
+    assert dev_n == "cuda"
+    assert rn.shape == (TOTAL, 8 * K) and sn.shape == (TOTAL, 8)
+    np.testing.assert_array_equal(rn, rg)
+    np.testing.assert_array_equal(sn, sg)
+    np.testing.assert_array_equal(rn[:, 6 * K:7 * K][:, -1], sn[:, 6])  # f of the last step, both packings

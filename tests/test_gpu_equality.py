@@ -150,3 +150,39 @@ def test_equality_rows_closed_loop_matches_per_step_launches(extra):
         np.testing.assert_array_equal(hist[k].cpu().numpy(), torch.stack(ref[k]).cpu().numpy(), err_msg=k)
     for k in ("u", "f"):
         assert _rel(hist[k].cpu().numpy(), torch.stack(ref[k]).cpu().numpy()) <= 1e-12, k
+
+
+def _pinned_z_draw(b, dz, k, n=32):
+    """Race Track 2 layout, N = 8, scenario b of `n` draws (seed 11): z at stage k pinned
+    to the start height + dz (lbg == ubg)."""
+    from nmpc_amd import make_spec, draw_scenarios
+    prob = orc.make_problem("race_track_2", N=8, T=0.2)
+    p = draw_scenarios(make_spec("race_track_2", N=8, T=0.2), n, seed=11)[b]
+    lbx, ubx, lbg, ubg = orc.bounds(prob)
+    lbg, ubg = lbg.copy(), ubg.copy()
+    lbg[k * prob.m] = ubg[k * prob.m] = p[2] + dz
+    return prob, p, lbx, ubx, lbg, ubg
+
+
+@pytest.mark.parametrize("b,dz,k", [(1, 3.0, 2), (1, 8.0, 4), (16, 3.0, 6), (28, 8.0, 6)])
+def test_watchdog_stop_with_equality_rows_matches_oracle(b, dz, k):
+    """The watchdog procedure (BacktrackingLineSearch::StartWatchDog / StopWatchDog) on a
+    problem with an equality row: after StopWatchDog the line search runs on the STORED
+    step, whose equality-multiplier component dy_c must come back with it (IPOPT keeps the
+    whole step in the watchdog's stored point; the kernel's weqy buffer).  These pinned
+    heights are out of reach, so the main phase shortens steps, the watchdog starts and is
+    stopped (1-4 times, counted by the oracle), and the solve ends in restoration with
+    Infeasible_Problem_Detected; GPU and oracle must take the same path: status and
+    iteration count equal."""
+    prob, p, lbx, ubx, lbg, ubg = _pinned_z_draw(b, dz, k)
+    ipo = orc.IpoptDense(prob, orc.REFERENCE_OPTS)
+    ref = ipo.solve(np.zeros(prob.nw), lbx, ubx, lbg, ubg, p)
+    assert ipo.wd_events["stop"] >= 1, ipo.wd_events  # the case exercises StopWatchDog
+    sol, st = _gpu_solve("race_track_2", 8, 0.2, np.zeros(prob.nw), lbx, ubx, lbg, ubg, p)
+    status, iters = int(np.ravel(st["status_code"])[0]), int(np.ravel(st["iter_count"])[0])
+    print(f"b={b} dz={dz} k={k}: watchdog {ipo.wd_events}; GPU status {status} iters {iters}, "
+          f"oracle {ref['status']} {ref['iter']}")
+    assert status == ref["status"]
+    assert iters == ref["iter"]
+    if status in (0, 1):
+        assert _rel(sol["x"].ravel(), ref["x"]) <= TOL
