@@ -165,12 +165,16 @@ int nmpc_solve_batch_dev(nmpc_handle* h, int32_t B,
                          int32_t* status, int32_t* iters, void* stream);
 
 /* Optional per-iteration trace (debugging / parity): when enabled, the next
- * solve records NMPC_TRACE_FIELDS doubles per iteration per scenario
- * {iter, mu, f_scaled, theta, delta_w, alpha_pr, alpha_du, ls_trials}
- * into a device buffer readable with nmpc_read_trace (host pointer,
+ * solve records NMPC_TRACE_FIELDS doubles per iteration per scenario into a
+ * device buffer readable with nmpc_read_trace (host pointer,
  * B x (max_iter+3) x NMPC_TRACE_FIELDS, row-major; the last three rows of each
- * scenario are reserved for diagnostic phase timers). */
-#define NMPC_TRACE_FIELDS 8
+ * scenario are reserved for diagnostic phase timers).  Row i holds
+ *   [0..7]  {iter, mu, f_scaled, theta, delta_w, alpha_pr, alpha_du, ls_trials}
+ *           after iteration i+1 (ls_trials < 0: a restoration iteration), and
+ *   [8..11] the main phase's convergence check at iteration count i:
+ *           {scaled NLP error, dual infeasibility / s_d, constraint violation,
+ *            complementarity / s_c} (IpoptCalculatedQuantities::curr_nlp_error). */
+#define NMPC_TRACE_FIELDS 12
 int nmpc_set_trace(nmpc_handle* h, int32_t enable);
 int nmpc_read_trace(nmpc_handle* h, int32_t B, double* host_out);
 

@@ -3054,6 +3054,10 @@ __device__ __forceinline__ int solve_one(Solver<CAP>& S, const Params* __restric
     double sc = nc ? (sumz + sumv) / nc : 0.0;
     sc = fmax(smax, sc) / smax;
     const double err = fmax(fmax(dinf / sd, cviol), cmp / sc);
+    if (trace && S.lanef() == 0) {  // the convergence check of iteration `it` (parity diagnostics)
+      double* t = trace + (long long)it * TRACE_F;
+      t[8] = err; t[9] = dinf / sd; t[10] = cviol; t[11] = cmp / sc;
+    }
     if (bad || !isfinite(err)) { status = ST_INVALID_NUMBER; break; }
     const double u_dinf = dinf / S.df, u_cmp = cmp / S.df;
     if (err <= o.tol && u_dinf <= o.dual_inf_tol && ucviol <= o.constr_viol_tol && u_cmp <= o.compl_inf_tol) {
@@ -3829,6 +3833,7 @@ struct SchedQ {
   int one_set;  // test hook (NMPC_SCHED_TEST_ONE_SET): only the waves on XCD 0 run, so
                 // sets 1..7 are never drained and the check must report it
   int hot_iters;  // a step after one with >= hot_iters iterations goes to the hot family (0: none)
+  int hot_prio;   // 1: a wave runs a step claimed from the hot family at raised issue priority
 };
 constexpr unsigned long long kSchedWaitTicks = 1000000000ull;  // s_memrealtime (100 MHz): 10 s
 
@@ -3865,7 +3870,7 @@ __global__ __launch_bounds__(WAVE, CAP::wpe) void nmpc_closed_loop_sched_kernel(
   const long long ro = fo * q.BX;  // ring offset of the hot family
   int jmin = 0;
   for (;;) {
-    int cb = -1, ck = -1;
+    int cb = -1, ck = -1, cf = 0;
     if (threadIdx.x == 0) {
       // Hot queues first, then normal ones, each lowest step first.  Finding nothing to
       // claim means every unfinished scenario of the set is running on some wave, so
@@ -3897,7 +3902,7 @@ __global__ __launch_bounds__(WAVE, CAP::wpe) void nmpc_closed_loop_sched_kernel(
             v = ld_acq(rg + (long long)j * q.BX + h);
           }
           if (v < 0) __hip_atomic_store(q.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          else { cb = v; ck = j; }
+          else { cb = v; ck = j; cf = f; }
           claimed = true;
           break;
         }
@@ -3905,7 +3910,15 @@ __global__ __launch_bounds__(WAVE, CAP::wpe) void nmpc_closed_loop_sched_kernel(
     }
     cb = __builtin_amdgcn_readfirstlane(cb);
     ck = __builtin_amdgcn_readfirstlane(ck);
+    cf = __builtin_amdgcn_readfirstlane(cf);
     if (ck < 0) break;
+    // a hot step (its predecessor ran long: restoration / max_iter) is likely on the chain
+    // that bounds the launch; its wave takes precedence over the CU's other waves at the
+    // issue ports they share (LDS, vector memory, scalar), which do not change results
+    if (q.hot_prio) {
+      if (cf) __builtin_amdgcn_s_setprio(2);
+      else __builtin_amdgcn_s_setprio(0);
+    }
     int its = 0;
     if (cb >= 0 && cb < B) {  // an out-of-range dispatch entry is claimed and skipped
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // the previous step's p, w (L1 invalidated)
@@ -4628,6 +4641,8 @@ int nmpc_closed_loop_dev(nmpc_handle* h, int32_t B, int32_t K, const double* lbx
     // hot family threshold: half of max_iter (NMPC_SCHED_HOT overrides; 0 = one family only)
     q.hot_iters = h->hp.o.max_iter / 2 > 0 ? h->hp.o.max_iter / 2 : 1;
     if (const char* hv = std::getenv("NMPC_SCHED_HOT")) q.hot_iters = std::atoi(hv);
+    q.hot_prio = 1;
+    if (const char* hp = std::getenv("NMPC_SCHED_PRIO")) q.hot_prio = std::atoi(hp) != 0;
     const char* one = std::getenv("NMPC_SCHED_TEST_ONE_SET");
     q.one_set = (one && std::atoi(one) != 0) ? 1 : 0;
     const long long n = (long long)NXCD * K * BX;

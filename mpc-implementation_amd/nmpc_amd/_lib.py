@@ -11,7 +11,7 @@ import os
 
 MAX_OBS = 16
 MAX_N = 63
-TRACE_FIELDS = 8
+TRACE_FIELDS = 12
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libnmpc_amd.so")

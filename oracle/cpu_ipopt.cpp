@@ -27,6 +27,8 @@
 #include <algorithm>
 #include <chrono>
 #include <cmath>
+#include <cstdio>
+#include <cstdlib>
 #include <cstdint>
 #include <cstring>
 #include <string>
@@ -723,6 +725,7 @@ struct Result {
 // oracle IpoptDense.solve, control flow restated statement by statement
 class Solver {
  public:
+  bool dbg_trace_ = std::getenv("NMPC_CPU_TRACE") != nullptr;
   Solver(const Prob& P, const Opts& o) : P_(P), o_(o) {
     n = P.n; m = P.m;
     ric.size(P);
@@ -802,6 +805,9 @@ class Solver {
           for (int r = c + 1; r < mc; ++r) L[r * mc + c2] -= (L[r * mc + c] * sgS[c]) * l2;
         }
       }
+      if (dbg_trace_)
+        std::fprintf(stderr, "cpu eq_schur dc %.3g nneg %d negS %d sing %d S00 %.6g\n", dcv, ric.nneg, negS, (int)sing,
+                     S[0]);
       if (sing) continue;
       if (negS != ric.nneg) return false;
       eqL = L; eqSg = sgS;
@@ -1646,6 +1652,12 @@ void Solver::solve(const double* w0p, const double* p, const double* lbxp, const
       vu[r] = sum_[r] ? std::max(std::min(vu[r], ks * mu / Ssu[r]), mu / (ks * Ssu[r])) : 0.0;
     }
     if (kind != K_RESTO) it += 1;
+    if (dbg_trace_) {  // NMPC_CPU_TRACE: per-iteration record on stderr (parity diagnostics)
+      double ymax = 0.0;
+      for (int r = 0; r < m; ++r) ymax = std::max(ymax, std::fabs(y[r]));
+      std::fprintf(stderr, "cpu it %d kind %d mu %.17g f %.17g delta %.6g alpha_p %.17g ls %d soc %d in_wd %d ymax %.6g\n",
+                   it, (int)kind, mu, f, delta_curr, alpha_p, ls_trials, (int)soc_taken, (int)in_wd, ymax);
+    }
     (void)soc_taken; (void)ls_trials; (void)have_wtri;
   }
   finish(x, it, status, zl, zu, y);

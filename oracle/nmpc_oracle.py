@@ -805,6 +805,7 @@ class IpoptDense:
         # active flag, trial iterations, the stored point / step / reference values
         wd_cnt, in_wd, wd_trial, wd_point, wd_alpha = 0, False, 0, None, 1.0
         self.wd_events = {"start": 0, "stop": 0, "success": 0, "resto_start": 0, "resto_stop": 0}
+        self.wd_stop_its = []  # main-phase iterations whose line search ran after StopWatchDog
         wd_trigger, wd_max = o["watchdog_shortened_iter_trigger"], o["watchdog_trial_iter_max"]
 
         def nlp_error(x_, s_, d_, gf_, J_, y_, zl_, zu_, vl_, vu_):
@@ -1507,6 +1508,7 @@ class IpoptDense:
                 x, s, y, zl, zu, vl, vu, ev, step, theta_ref, phi_ref, gBD = wd_point
                 f, d, gf, J = df * ev.F, dc * ev.g, df * ev.gradF, dc[:, None] * ev.J
                 in_wd, wd_cnt, tiny = False, 0, False
+                self.wd_stop_its.append(it + 1)
             if wd_trigger > 0 and not in_wd and not tiny and not in_soft_resto and wd_cnt >= wd_trigger:
                 # StartWatchDog: store the iterate, its step and the reference values
                 wd_point = (x, s, y, zl, zu, vl, vu, ev, step, theta_ref, phi_ref, gBD)
@@ -1549,6 +1551,7 @@ class IpoptDense:
                         f, d, gf, J = df * ev.F, dc * ev.g, df * ev.gradF, dc[:, None] * ev.J
                         in_wd, wd_cnt, skip_first = False, 0, True
                         self.wd_events["stop"] += 1
+                        self.wd_stop_its.append(it + 1)
                         continue
                     # a watchdog trial iteration: the full step is taken unchecked
                     accepted = ("reg", frac_to_bound(tau, x, s, step[0], step[1]), step, wtri)
@@ -1616,7 +1619,8 @@ class IpoptDense:
                 it += 1
             if trace and accepted[0] != "resto":
                 tr.append(dict(iter=it, mu=mu, f=f, theta=float(np.sum(np.abs(d - s))), delta=delta_curr,
-                               alpha_p=alpha_p, alpha_d=alpha_d, ls=ls_trials, soc=soc_taken))
+                               alpha_p=alpha_p, alpha_d=alpha_d, ls=ls_trials, soc=soc_taken,
+                               ymax=float(np.max(np.abs(y))) if len(y) else 0.0))
 
         return self._result(x, w0, it, status, df, dc, zl, zu, y, lbx, ubx, tr, mu=mu)
 
