@@ -138,11 +138,11 @@ int nmpc_dims(const nmpc_handle* h, int32_t* nw, int32_t* ng, int32_t* np, int32
  * Bounds as IPOPT reads them: |b| >= 1e19 is no bound; lbx == ubx fixes a variable
  * (fixed_variable_treatment = make_parameter: held at the bound, no step, lam_x 0);
  * rows with lbg == ubg are IPOPT's equality constraints c(x) = g(x) - lbg = 0 (no slack,
- * no relaxation; augmented-system step with IPOPT's inertia test), up to 16
+ * no relaxation; augmented-system step with IPOPT's inertia test), up to 64
  * per scenario.  A batch with any equality row runs on the equality class (global rows,
  * any shape): the host enqueues a bounds scan and both classes, and a device flag lets
  * exactly one of them run (no host round trip; the same for the _dev entry points).
- * lbx > ubx, more than 16 equality rows, or equality rows with the fp32 Riccati leg
+ * lbx > ubx, more than 64 equality rows, or equality rows with the fp32 Riccati leg
  * report status -11 (IPOPT Invalid_Problem_Definition) for that scenario. */
 int nmpc_solve_batch(nmpc_handle* h, int32_t B,
                      const double* x0, int64_t ld_x0,

@@ -50,8 +50,8 @@ constexpr double BIGB = 1e19;  // IPOPT nlp_{lower,upper}_bound_inf
 constexpr int FCAP = 128;      // filter capacity (>= max_iter of the reference opts)
 constexpr int TRACE_F = NMPC_TRACE_FIELDS;
 // equality rows (lbg == ubg) per problem the augmented-system (Schur complement) step
-// supports; more report Invalid_Problem_Definition (-11)
-#define NMPC_MEQ 16
+// supports (lane l owns rows l and l + 64 of S); more report Invalid_Problem_Definition (-11)
+#define NMPC_MEQ 128
 
 // ---- status codes (IPOPT ApplicationReturnStatus) ----
 constexpr int ST_SUCCESS = 0, ST_ACCEPTABLE = 1, ST_INFEASIBLE = 2, ST_TINY = 3, ST_MAXITER = -1,
@@ -135,7 +135,8 @@ constexpr Lay make_layout(int N, int m, bool lr, bool refine, bool eq) {
   L.wds = g; g += al8(ng); L.wpR = g; g += al8(ng); L.wnR = g; g += al8(ng); L.wzpR = g; g += al8(ng);
   L.wznR = g; g += al8(ng); L.wdpR = g; g += al8(ng); L.wdnR = g; g += al8(ng); L.wdyR = g; g += al8(ng);
   if (eq) {  // equality rows (the equality class only)
-    L.eqi = g; g += al8(NMPC_MEQ / 2 + 1); L.eqS = g; g += al8(NMPC_MEQ * NMPC_MEQ + NMPC_MEQ);
+    // eqS: S (column-major, NMPC_MEQ x NMPC_MEQ), its signed factor (same layout), pivot signs
+    L.eqi = g; g += al8(NMPC_MEQ / 2 + 1); L.eqS = g; g += al8(2 * NMPC_MEQ * NMPC_MEQ + NMPC_MEQ);
     L.eqy = g; g += al8(ng); L.eqy2 = g; g += al8(ng); L.weqy = g; g += al8(ng);
   }
   if (!lr) { L.kf = g; g += al8(6 * N); }
@@ -956,116 +957,170 @@ struct Solver {
     sync();
   }
   // Schur complement S = J_c H^-1 J_c^T of the equality rows from meq unit solves, and its
-  // signed Cholesky factor (lane l holds row l) with delta_c = 0, then IPOPT's
-  // jacobian_regularization_value * mu^0.25 if S is singular.  Inertia test (Haynsworth):
-  // the augmented system [H J_c^T; J_c -delta_c I] has n positive and meq negative
-  // eigenvalues iff S + delta_c I has exactly as many negative pivots as the Riccati sweep
-  // had (nneg).  The factor and the pivot signs go to eqS for the step's solves.
+  // signed Cholesky factor with delta_c = 0, then IPOPT's jacobian_regularization_value *
+  // mu^0.25 if S is singular.  Inertia test (Haynsworth): the augmented system
+  // [H J_c^T; J_c -delta_c I] has n positive and meq negative eigenvalues iff S + delta_c I
+  // has exactly as many negative pivots as the Riccati sweep had (nneg).
+  // Storage (eqS, workspace): S and the factor column-major, MQ = NMPC_MEQ rows per column;
+  // lane l owns rows l + 64 q (slots q < EQR) of every column, so every access is a lane's
+  // own entry and the pivot column reaches the other lanes by readlane.
   // (allow_dc false: the least-squares multipliers, which IPOPT computes without
   // regularisation -- a singular S there means y = 0)
-  __device__ __forceinline__ bool eq_schur(double mu_, bool allow_dc = true) {
-    const int ln = lanef();
-    double row[NMPC_MEQ];
+  static constexpr int EQR = NMPC_MEQ / WAVE;
+  // entry `row` (wave-uniform) of a per-lane slot vector v[EQR]
+  __device__ __forceinline__ static double eq_bcast(const double* v, int row) {
+    double r = 0.0;
 #pragma unroll
-    for (int c = 0; c < NMPC_MEQ; ++c) row[c] = 0.0;
+    for (int q = 0; q < EQR; ++q)
+      if ((row >> 6) == q) r = readlane_d(v[q], row & (WAVE - 1));
+    return r;
+  }
+  __device__ __forceinline__ bool eq_schur(double mu_, bool allow_dc = true) {
+    constexpr int MQ = NMPC_MEQ;
+    const int ln = lanef();
+    GLB double* Sm = eqS_();
+    GLB double* Fm = Sm + MQ * MQ;
+    GLB double* sgm = Fm + MQ * MQ;
     for (int e = 0; e < meq; ++e) {
       const int re = eqi_()[e];
       double g8[8];
       row_grad8(re, g8);
       resolve_eq(ru, re / m, g8);
       forward(dUr, Xt);  // -H^-1 J_e^T (the fp64 classes' refinement buffer; Xt is free here)
-      const double se = ln < meq ? -row_jd(eqi_()[ln < meq ? ln : 0], Xt) : 0.0;
 #pragma unroll
-      for (int c = 0; c < NMPC_MEQ; ++c)
-        if (c == e) row[c] = se;
+      for (int q = 0; q < EQR; ++q) {
+        const int l = ln + q * WAVE;
+        const double se = l < meq ? -row_jd(eqi_()[l < meq ? l : 0], Xt) : 0.0;
+        if (l < meq) Sm[e * MQ + l] = se;  // S[l][e]
+      }
       sync();
     }
-    double scale = 0.0;
+    double dmax = 0.0;
 #pragma unroll
-    for (int c = 0; c < NMPC_MEQ; ++c)
-      if (c < meq) scale = fmax(scale, fabs(readlane_d(row[c], c)));
+    for (int q = 0; q < EQR; ++q) {
+      const int l = ln + q * WAVE;
+      if (l < meq) dmax = fmax(dmax, fabs(Sm[l * MQ + l]));
+    }
+    const double scale = wmax(dmax);
     for (int att = 0; att < (allow_dc ? 2 : 1); ++att) {
       const double dcv = att == 0 ? 0.0 : 1e-8 * pow(mu_, 0.25);
-      double L[NMPC_MEQ], sgS[NMPC_MEQ];
+      for (int c = 0; c < meq; ++c) {
 #pragma unroll
-      for (int c = 0; c < NMPC_MEQ; ++c) L[c] = row[c] + ((c == ln) ? dcv : 0.0);
+        for (int q = 0; q < EQR; ++q) {
+          const int l = ln + q * WAVE;
+          if (l < meq) Fm[c * MQ + l] = Sm[c * MQ + l] + ((c == l) ? dcv : 0.0);
+        }
+      }
+      sync();
       bool sing = false;
       int negS = 0;
+      double sgl[EQR];  // slot q of lane l: the sign of pivot l + 64 q
 #pragma unroll
-      for (int c = 0; c < NMPC_MEQ; ++c) {
-        sgS[c] = 1.0;
-        if (c < meq) {
-          const double d = readlane_d(L[c], c);
-          if (!(fabs(d) > 1e-14 * scale)) sing = true;
-          sgS[c] = d < 0.0 ? -1.0 : 1.0;
-          negS += d < 0.0 ? 1 : 0;
-          const double ig = rsq(fabs(d));
-          const double Lcc = fabs(d) * ig;
-          L[c] = (ln == c) ? Lcc : ((ln > c) ? (L[c] * ig) * sgS[c] : L[c]);
+      for (int q = 0; q < EQR; ++q) sgl[q] = 1.0;
+      for (int c = 0; c < meq; ++c) {
+        double col[EQR], lc[EQR];
 #pragma unroll
-          for (int c2 = c + 1; c2 < NMPC_MEQ; ++c2) {
-            if (c2 < meq) {
-              const double Lc2c = readlane_d(L[c], c2);
-              if (ln > c) L[c2] -= (L[c] * sgS[c]) * Lc2c;
+        for (int q = 0; q < EQR; ++q) {
+          const int l = ln + q * WAVE;
+          col[q] = l < meq ? Fm[c * MQ + l] : 0.0;
+        }
+        const double d = eq_bcast(col, c);
+        if (!(fabs(d) > 1e-14 * scale)) sing = true;
+        const double sgc = d < 0.0 ? -1.0 : 1.0;
+        negS += d < 0.0 ? 1 : 0;
+        const double ig = rsq(fabs(d));
+        const double Lcc = fabs(d) * ig;
+#pragma unroll
+        for (int q = 0; q < EQR; ++q) {
+          const int l = ln + q * WAVE;
+          if (l == c) sgl[q] = sgc;
+          lc[q] = (l == c) ? Lcc : ((l > c) ? (col[q] * ig) * sgc : col[q]);
+          if (l < meq) Fm[c * MQ + l] = lc[q];
+        }
+        // right-looking update of the lane's own trailing entries (rows > c), eight
+        // columns per batch (their loads issued together)
+        for (int c2 = c + 1; c2 < meq; c2 += 8) {
+#pragma unroll
+          for (int q = 0; q < EQR; ++q) {
+            const int l = ln + q * WAVE;
+            if ((q + 1) * WAVE <= c + 1) continue;  // wave-uniform: no row of this slot is > c
+            const double lcs = lc[q] * sgc;
+            double v[8];
+#pragma unroll
+            for (int t = 0; t < 8; ++t) v[t] = (l < meq && c2 + t < meq) ? Fm[(c2 + t) * MQ + l] : 0.0;
+#pragma unroll
+            for (int t = 0; t < 8; ++t) {
+              if (c2 + t < meq) {
+                const double Lc2c = eq_bcast(lc, c2 + t);
+                if (l < meq && l > c) Fm[(c2 + t) * MQ + l] = v[t] - lcs * Lc2c;
+              }
             }
           }
         }
+        sync();
       }
       if (sing) continue;
       if (negS != nneg) return false;
-      if (ln < meq) {
 #pragma unroll
-        for (int c = 0; c < NMPC_MEQ; ++c) eqS_()[ln * NMPC_MEQ + c] = L[c];
-      }
-      if (ln == 0) {
-#pragma unroll
-        for (int c = 0; c < NMPC_MEQ; ++c) eqS_()[NMPC_MEQ * NMPC_MEQ + c] = sgS[c];
+      for (int q = 0; q < EQR; ++q) {
+        const int l = ln + q * WAVE;
+        if (l < meq) sgm[l] = sgl[q];
       }
       sync();
       return true;
     }
     return false;
   }
-  // dy = (S + delta_c I)^-1 rhs with the stored factor (rhs: lane e holds entry e); every
-  // lane returns the full solution in lane-e order through readlane-able registers
-  __device__ __forceinline__ double eq_solve(double rhs) const {
+  // dy = (S + delta_c I)^-1 rhs with the stored factor (rhs[q]: lane l holds entry l + 64 q);
+  // the solution comes back in the same slots
+  __device__ __forceinline__ void eq_solve(const double* rhs, double* out) const {
+    constexpr int MQ = NMPC_MEQ;
     const int ln = lanef();
-    double L[NMPC_MEQ], sgS[NMPC_MEQ];
+    const GLB double* Fm = eqS_() + MQ * MQ;
+    const GLB double* sgm = Fm + MQ * MQ;
+    double sgl[EQR], part[EQR], zl[EQR], yl[EQR];
 #pragma unroll
-    for (int c = 0; c < NMPC_MEQ; ++c) {
-      L[c] = (ln < meq) ? eqS_()[(ln < meq ? ln : 0) * NMPC_MEQ + c] : 0.0;
-      sgS[c] = eqS_()[NMPC_MEQ * NMPC_MEQ + c];
+    for (int q = 0; q < EQR; ++q) {
+      const int l = ln + q * WAVE;
+      sgl[q] = l < meq ? sgm[l] : 1.0;
+      part[q] = l < meq ? rhs[q] : 0.0;
+      zl[q] = 0.0;
+      yl[q] = 0.0;
     }
-    // L z = rhs (column-oriented: lane l keeps its partial sum)
-    double part = ln < meq ? rhs : 0.0;
-    double z[NMPC_MEQ];
+    // L z = rhs (column-oriented: each row keeps its partial sum; row c ends with z_c)
+    for (int c = 0; c < meq; ++c) {
+      double col[EQR];
 #pragma unroll
-    for (int c = 0; c < NMPC_MEQ; ++c) {
-      z[c] = 0.0;
-      if (c < meq) {
-        const double Lcc = readlane_d(L[c], c);
-        z[c] = readlane_d(part, c) / Lcc;
-        if (ln > c) part -= L[c] * z[c];
+      for (int q = 0; q < EQR; ++q) {
+        const int l = ln + q * WAVE;
+        col[q] = l < meq ? Fm[c * MQ + l] : 0.0;
+      }
+      const double Lcc = eq_bcast(col, c);
+      const double zc = eq_bcast(part, c) / Lcc;
+#pragma unroll
+      for (int q = 0; q < EQR; ++q) {
+        const int l = ln + q * WAVE;
+        if (l == c) zl[q] = zc;
+        if (l > c) part[q] -= col[q] * zc;
       }
     }
-    // L^T dy = Sigma z (every lane, broadcast entries)
-    double y[NMPC_MEQ];
+    // L^T dy = Sigma z, back to front (every lane forms each entry; row c keeps y_c)
+    for (int c = meq - 1; c >= 0; --c) {
+      double col[EQR];
 #pragma unroll
-    for (int c = NMPC_MEQ - 1; c >= 0; --c) {
-      y[c] = 0.0;
-      if (c < meq) {
-        double a = sgS[c] * z[c];
-#pragma unroll
-        for (int j = c + 1; j < NMPC_MEQ; ++j)
-          if (j < meq) a -= readlane_d(L[c], j) * y[j];
-        y[c] = a / readlane_d(L[c], c);
+      for (int q = 0; q < EQR; ++q) {
+        const int l = ln + q * WAVE;
+        col[q] = l < meq ? Fm[c * MQ + l] : 0.0;
       }
-    }
-    double out = 0.0;
+      double a = eq_bcast(sgl, c) * eq_bcast(zl, c);
+      for (int j = c + 1; j < meq; ++j) a -= eq_bcast(col, j) * eq_bcast(yl, j);
+      const double yc = a / eq_bcast(col, c);
 #pragma unroll
-    for (int c = 0; c < NMPC_MEQ; ++c)
-      if (c == ln) out = y[c];
-    return out;
+      for (int q = 0; q < EQR; ++q)
+        if (ln + q * WAVE == c) yl[q] = yc;
+    }
+#pragma unroll
+    for (int q = 0; q < EQR; ++q) out[q] = yl[q];
   }
   // the step with the equality rows: base solve (dUo, dXo) with the assembled terms, then
   // dy = (S + delta_c)^-1 (c + J_c dX0), q += J_c^T dy, solve again (Newton / SOC step);
@@ -1079,20 +1134,28 @@ struct Solver {
     const double g0[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     resolve_eq(rv, -1, g0);
     forward(dUo, dXo);
-    const int re = eqi_()[ln < meq ? ln : 0];
-    const double jd = row_jd(re, dXo);
-    double rhs;
-    if constexpr (MODE == 0) rhs = (d[re] - s[re]) + jd;
-    else if constexpr (MODE == 1) rhs = dms[re] + jd;
-    else rhs = -jd;
-    const double dy = eq_solve(rhs);
-    if (ln < meq) dyo[re] = dy;
+    double rhs[EQR], dy[EQR];
+#pragma unroll
+    for (int q = 0; q < EQR; ++q) {
+      const int l = ln + q * WAVE;
+      const int re = eqi_()[l < meq ? l : 0];
+      const double jd = row_jd(re, dXo);
+      if constexpr (MODE == 0) rhs[q] = (d[re] - s[re]) + jd;
+      else if constexpr (MODE == 1) rhs[q] = dms[re] + jd;
+      else rhs[q] = -jd;
+    }
+    eq_solve(rhs, dy);
+#pragma unroll
+    for (int q = 0; q < EQR; ++q) {
+      const int l = ln + q * WAVE;
+      if (l < meq) dyo[eqi_()[l]] = dy[q];
+    }
     // q_k += (+-) dy_e g8_e at each row's stage (serial over the rows: rows may share a stage)
     for (int e = 0; e < meq; ++e) {
       const int r = eqi_()[e];
       double g8[8];
       row_grad8(r, g8);
-      const double de = readlane_d(dy, e) * (MODE == 2 ? -1.0 : 1.0);
+      const double de = eq_bcast(dy, e) * (MODE == 2 ? -1.0 : 1.0);
       const int k = r / m;
       if (ln < 8) {
         double gv = 0.0;
@@ -1722,10 +1785,14 @@ struct Solver {
     STAMP1(PH_FWD);
   }
 
-  // ds_r = Gt_r dX_k + rd_r (J dU = G Z dU = G dX)
-  __device__ __forceinline__ void row_step(const LDS double* dXs, const GLB double* rdsrc, bool rd_is_dms, RV* dso) {
+  // second-order correction's row step ds_r = Gt_r dX_k + dms_r (J dU = G Z dU = G dX),
+  // and the primal fraction to the boundary of the step (dUs, ds) in the same pass
+  // (frac_to_bound: the same expressions; min over the rows and controls)
+  __device__ __forceinline__ double row_step_soc(const LDS double* dXs, const GLB double* dUs, RV* dso,
+                                                 double tau_) {
     STAMP0();
-    for (int r = lanef(); r < ng; r += WAVE) {
+    double a = 1.0;
+    rows([&](int r, bool on) {
       const int k = r / m, i = r - k * m;
       const LDS double* xk = X + k * 8;
       const LDS double* dxk = dXs + k * 8;
@@ -1738,20 +1805,36 @@ struct Solver {
         const double idd = rsq(ddx * ddx + ddy * ddy);
         jd = dc[r] * ((-(ddx * idd)) * dxk[0] + (-(ddy * idd)) * dxk[1]);
       }
-      const double rd = rd_is_dms ? rdsrc[r] : d[r] - s[r];
-      dso[r] = eqr(r) ? 0.0 : jd + rd;  // equality rows: the slack stays at the target
+      const double lo = dl[r], hi = du[r], sr = s[r];
+      const double dd = eqlo(lo) ? 0.0 : jd + dms[r];  // equality rows: the slack stays at the target
+      if (on) dso[r] = dd;
+      const double al = (-tau_ * (sr - lo)) / dd, au = (-tau_ * (hi - sr)) / (-dd);
+      if (on && hasl(lo) && dd < 0) a = fmin(a, al);
+      if (on && hasu(hi) && -dd < 0) a = fmin(a, au);
+    });
+    for (int i = lanef(); i < nw; i += WAVE) {
+      const double dx = dUs[i];
+      if (hasl(xl[i]) && dx < 0) a = fmin(a, (-tau_ * (U[i] - xl[i])) / dx);
+      if (hasu(xu[i]) && -dx < 0) a = fmin(a, (-tau_ * (xu[i] - U[i])) / (-dx));
     }
+    a = wmin(a);
     STAMP1(PH_ROWSTEP);
     sync();
+    return a;
   }
 
   // Newton-direction row step fused with the line-search set-up sums over the
   // same rows: theta = sum |d - s|, the slack part of grad(phi)^T d, and the
   // tiny-step ratio max |ds| / (1 + |s|) (per-lane partials; caller reduces)
-  __device__ __forceinline__ void row_step_ls(const LDS double* dXs, double mu_, double& th, double& g, double& msv) {
+  // The same pass also forms the row parts of the step's primal and dual fraction-to-the-
+  // boundary (frac_to_bound_x / dual_frac_to_bound_x with tau_, mu_: the same expressions,
+  // per-lane partial minima ap / ad, caller reduces), which the line search and the accept
+  // pass would otherwise each recompute in a pass of their own.
+  __device__ __forceinline__ void row_step_ls(const LDS double* dXs, double mu_, double tau_, double& th, double& g,
+                                              double& msv, double& ap, double& ad) {
     STAMP0();
     const double kd = P->o.kappa_d;
-    th = 0.0; g = 0.0; msv = 0.0;
+    th = 0.0; g = 0.0; msv = 0.0; ap = 1.0; ad = 1.0;
     rows([&](int r, bool on) {
       const int k = r / m, i = r - k * m;
       const double dcr = dc[r], sr = s[r], dr = d[r], lo = dl[r], hi = du[r];
@@ -1776,6 +1859,18 @@ struct Solver {
         g += gs * dsr;
         msv = fmax(msv, fabs(dsr / (1.0 + fabs(sr))));
       }
+      // fraction to the boundary of this step: primal (frac_to_bound_x) ...
+      const double al = (-tau_ * (sr - lo)) / dsr, au = (-tau_ * (hi - sr)) / (-dsr);
+      if (on && hl && dsr < 0) ap = fmin(ap, al);
+      if (on && hu && -dsr < 0) ap = fmin(ap, au);
+      // ... and dual (dual_frac_to_bound_x: dv_s with mu_)
+      const double vlr = vl[r], vur = vu[r];
+      double a1 = 0.0, a2 = 0.0;
+      if (hl) { const double iS = rcp(sr - lo); a1 = mu_ * iS - vlr - vlr * iS * dsr; }
+      if (hu) { const double iS = rcp(hi - sr); a2 = mu_ * iS - vur + vur * iS * dsr; }
+      const double b1 = (-tau_ * vlr) / a1, b2 = (-tau_ * vur) / a2;
+      if (on && hl && a1 < 0) ad = fmin(ad, b1);
+      if (on && hu && a2 < 0) ad = fmin(ad, b2);
     });
     STAMP1(PH_ROWSTEP);
     sync();
@@ -1811,10 +1906,15 @@ struct Solver {
   }
   // restoration step rows: dy, dp, dn, ds (= J dx + c - dp + dn); for the Newton
   // direction also theta_R and the slack/p/n part of grad(phi_R)^T d
+  // The pass also forms the row part of the step's primal fraction to the boundary
+  // (frac_to_bound_resto with tau_) and, for the Newton direction (!soc), of its dual one
+  // (dual_frac_to_bound_resto with the current mu): per-lane partial minima ap / ad, the
+  // caller adds the controls and reduces.
   __device__ __forceinline__ void row_step_resto(const LDS double* dXs, bool soc, RV* dso, GLB double* dpo,
-                                                 GLB double* dno, GLB double* dyo, double& th, double& gsum) {
+                                                 GLB double* dno, GLB double* dyo, double& th, double& gsum,
+                                                 double tau_, double& ap, double& ad) {
     const double kd = P->o.kappa_d;
-    th = 0.0; gsum = 0.0;
+    th = 0.0; gsum = 0.0; ap = 1.0; ad = 1.0;
     rows([&](int r, bool on) {
       const int k = r / m, i = r - k * m;
       const LDS double* xk = X + k * 8;
@@ -1836,9 +1936,18 @@ struct Solver {
       const double dpv = (dyv - rp) / Sp, dnv = (-dyv - rn) / Sn;
       const double dsv = eqr(r) ? 0.0 : jd + c - dpv + dnv;
       if (on) { dso[r] = dsv; dpo[r] = dpv; dno[r] = dnv; dyo[r] = dyv; }
+      const double lo = dl[r], hi = du[r], sr = s[r];
+      const bool hl = hasl(lo), hu = hasu(hi);
+      // primal fraction to the boundary (frac_to_bound_x rows + the p, n bounds)
+      {
+        const double al = (-tau_ * (sr - lo)) / dsv, au = (-tau_ * (hi - sr)) / (-dsv);
+        if (on && hl && dsv < 0) ap = fmin(ap, al);
+        if (on && hu && -dsv < 0) ap = fmin(ap, au);
+        const double bp = (-tau_ * pr) / dpv, bn = (-tau_ * nr) / dnv;
+        if (on && dpv < 0) ap = fmin(ap, bp);
+        if (on && dnv < 0) ap = fmin(ap, bn);
+      }
       if (!soc) {
-        const double lo = dl[r], hi = du[r], sr = s[r];
-        const bool hl = hasl(lo), hu = hasu(hi);
         const double gs = -(hl ? mu / (sr - lo) : 0.0) + (hu ? mu / (hi - sr) : 0.0) +
                           kd * mu * ((hl && !hu ? 1.0 : 0.0) - (hu && !hl ? 1.0 : 0.0));
         const double gr = gs * dsv + (rho - mu / pr + kd * mu) * dpv + (rho - mu / nr + kd * mu) * dnv;
@@ -1846,6 +1955,20 @@ struct Solver {
           th += fabs(c);
           gsum += gr;
         }
+        // dual fraction to the boundary (dual_frac_to_bound_x rows with dv_s, + the p, n
+        // multipliers)
+        const double vlr = vl[r], vur = vu[r], zp = zpR[r], zn = znR[r];
+        double a1 = 0.0, a2 = 0.0;
+        if (hl) { const double iS = rcp(sr - lo); a1 = mu * iS - vlr - vlr * iS * dsv; }
+        if (hu) { const double iS = rcp(hi - sr); a2 = mu * iS - vur + vur * iS * dsv; }
+        const double b1 = (-tau_ * vlr) / a1, b2 = (-tau_ * vur) / a2;
+        if (on && hl && a1 < 0) ad = fmin(ad, b1);
+        if (on && hu && a2 < 0) ad = fmin(ad, b2);
+        const double dzp = mu / pr - zp - (zp / pr) * dpv;
+        const double dzn = mu / nr - zn - (zn / nr) * dnv;
+        const double cp = (-tau_ * zp) / dzp, cn = (-tau_ * zn) / dzn;
+        if (on && dzp < 0) ad = fmin(ad, cp);
+        if (on && dzn < 0) ad = fmin(ad, cn);
       }
     });
     sync();
@@ -2238,12 +2361,9 @@ __device__ __forceinline__ void resto_phase(const Params* __restrict__ prm, doub
         const bool cachedR = !firstR;
         // ---- progress w.r.t. the original problem (RestoConvergenceCheck)
         if (!firstR) {
-          double tho = 0.0;
-          S.rows([&](int r, bool on) {
-            const double t = fabs(S.d[r] - S.s[r]);
-            if (on) tho += t;
-          });
-          tho = wsum(tho);
+          // sum |d - s| of the current iterate: formed by the accept pass that produced it
+          // (the same rows in the same per-lane order, so the same bits)
+          const double tho = V[22];
           S.mu = V[0];
           const double pho = S.phi_of(V[12], S.rvars[32], S.rvars[33]);
           S.mu = V[4];
@@ -2413,13 +2533,30 @@ __device__ __forceinline__ void resto_phase(const Params* __restrict__ prm, doub
         if (!fok) { rstat = ST_STEP_ERR; break; }
         S.forward(S.dU, S.dX);
         S.refine(S.sigx, S.ru, S.dU, S.dX);
+        // primal / dual fraction to the boundary of the Newton step, formed with its row pass
+        // (valid until the watchdog restores another iterate and step)
+        double rftb_p = 1.0, rftb_d = 1.0;
+        bool rftb_ok = true;
         {
           STAMP0();
-          double th, g;
-          S.row_step_resto(S.dX, false, S.ds, S.dpR, S.dnR, S.dyR, th, g);
-          for (int i = S.lanef(); i < nw; i += WAVE) g += S.ru[i] * S.dU[i];
+          double th, g, ap, ad;
+          const double tauR = V[5];
+          S.row_step_resto(S.dX, false, S.ds, S.dpR, S.dnR, S.dyR, th, g, tauR, ap, ad);
+          for (int i = S.lanef(); i < nw; i += WAVE) {
+            const double du_ = S.dU[i];
+            g += S.ru[i] * du_;
+            const double ui = S.U[i], xli = S.xl[i], xui = S.xu[i];
+            if (S.hasl(xli) && du_ < 0) ap = fmin(ap, (-tauR * (ui - xli)) / du_);
+            if (S.hasu(xui) && -du_ < 0) ap = fmin(ap, (-tauR * (xui - ui)) / (-du_));
+            double a1, a2;
+            S.dz_x(i, du_, a1, a2);
+            if (S.hasl(xli) && a1 < 0) ad = fmin(ad, (-tauR * S.zl[i]) / a1);
+            if (S.hasu(xui) && a2 < 0) ad = fmin(ad, (-tauR * S.zu[i]) / a2);
+          }
           V[15] = wsum(th);
           V[16] = wsum(g);
+          rftb_p = wmin(ap);
+          rftb_d = wmin(ad);
           STAMP1(PH_ROWSTEP);
         }
         V[17] = cachedR ? S.phi_of(0.0, S.rvars[32], S.rvars[33]) + S.pn_of(S.rvars[34], S.rvars[35], S.rvars[36])
@@ -2459,7 +2596,7 @@ __device__ __forceinline__ void resto_phase(const Params* __restrict__ prm, doub
             S.wpR[r] = S.pR[r]; S.wnR[r] = S.nR[r]; S.wzpR[r] = S.zpR[r]; S.wznR[r] = S.znR[r];
             S.wdpR[r] = S.dpR[r]; S.wdnR[r] = S.dnR[r]; S.wdyR[r] = S.dyR[r];
           }
-          const double at = S.frac_to_bound_resto(V[5], S.dU, S.ds, S.dpR, S.dnR);
+          const double at = rftb_ok ? rftb_p : S.frac_to_bound_resto(V[5], S.dU, S.ds, S.dpR, S.dnR);
           WD[0] = V[15]; WD[1] = V[16]; WD[2] = V[17]; WD[3] = at; WD[4] = V[4]; WD[5] = S.delta;
           sync();
           rin_wd = true;
@@ -2482,6 +2619,7 @@ __device__ __forceinline__ void resto_phase(const Params* __restrict__ prm, doub
           V[15] = WD[0]; V[16] = WD[1]; V[17] = WD[2];
           S.delta = WD[5];
           rwd_dir = true;
+          rftb_ok = false;
           rin_wd = false;
           rwd_cnt = 0;
         };
@@ -2491,7 +2629,7 @@ __device__ __forceinline__ void resto_phase(const Params* __restrict__ prm, doub
         double a = 0.0, a_test = 0.0;
         bool rskip = false, rforced = false;
        while (true) {
-        V[18] = S.frac_to_bound_resto(V[5], S.dU, S.ds, S.dpR, S.dnR);
+        V[18] = rftb_ok ? rftb_p : S.frac_to_bound_resto(V[5], S.dU, S.ds, S.dpR, S.dnR);
         if (rin_wd) {
           double fo_t, ph, th;
           const bool ok_t = S.trial_resto(V[18], S.dU, S.ds, S.dpR, S.dnR, fo_t, ph, th);
@@ -2536,8 +2674,15 @@ __device__ __forceinline__ void resto_phase(const Params* __restrict__ prm, doub
               S.forward(S.dU2, S.dX);
               S.refine(S.sigx, S.ru, S.dU2, S.dX);
               double t0, t1;
-              S.row_step_resto(S.dX, true, S.ds2, S.dp2R, S.dn2R, S.dy2R, t0, t1);
-              a_soc = S.frac_to_bound_resto(V[5], S.dU2, S.ds2, S.dp2R, S.dn2R);
+              double ap, u1;
+              const double tauR = V[5];
+              S.row_step_resto(S.dX, true, S.ds2, S.dp2R, S.dn2R, S.dy2R, t0, t1, tauR, ap, u1);
+              for (int i = S.lanef(); i < nw; i += WAVE) {  // frac_to_bound_resto's control part
+                const double du_ = S.dU2[i], ui = S.U[i], xli = S.xl[i], xui = S.xu[i];
+                if (S.hasl(xli) && du_ < 0) ap = fmin(ap, (-tauR * (ui - xli)) / du_);
+                if (S.hasu(xui) && -du_ < 0) ap = fmin(ap, (-tauR * (xui - ui)) / (-du_));
+              }
+              a_soc = wmin(ap);
               dsp = S.ds2; dpp = S.dp2R; dnp = S.dn2R;
               double fo2, ph2, th2;
               if (!S.trial_resto(a_soc, S.dU2, S.ds2, S.dp2R, S.dn2R, fo2, ph2, th2)) break;
@@ -2571,7 +2716,8 @@ __device__ __forceinline__ void resto_phase(const Params* __restrict__ prm, doub
           // ---- accept the restoration trial point (the step's dual components with its
           //      own mu, the kappa_sigma safeguard with the current one)
           if (rwd_dir) S.mu = WD[4];
-          const double ad = S.dual_frac_to_bound_resto(V[5], dUa, dsa, dpa, dna);
+          const double ad = (acc == 1 && rftb_ok && !rwd_dir) ? rftb_d
+                                                               : S.dual_frac_to_bound_resto(V[5], dUa, dsa, dpa, dna);
           for (int i = S.lanef(); i < nw; i += WAVE) {
             double dzl, dzu;
             S.dz_x(i, dUa[i], dzl, dzu);
@@ -2585,6 +2731,7 @@ __device__ __forceinline__ void resto_phase(const Params* __restrict__ prm, doub
           }
           const double muR = V[4], aP = V[19];  // volatile LDS scalars read once
           const double dmuR = rwd_dir ? (double)WD[4] : muR;
+          double tho = 0.0;  // theta of the original problem at the new iterate (next check)
           S.rows([&](int r, bool on) {
             const double sr = S.s[r], lo = S.dl[r], hi = S.du[r], vlr = S.vl[r], vur = S.vu[r];
             const double dsr = dsa[r], dpr = dpa[r], dnr = dna[r], dyr = dya[r];
@@ -2605,14 +2752,18 @@ __device__ __forceinline__ void resto_phase(const Params* __restrict__ prm, doub
             const double nzp = zp + ad * dzp, nzn = zn + ad * dzn;
             const double zpn = fmax(fmin(nzp, ks * muR / pn), muR / (ks * pn));
             const double znn = fmax(fmin(nzn, ks * muR / nn), muR / (ks * nn));
+            const double t = fabs(dtr - sn);
             if (on) {
               S.zpR[r] = zpn; S.znR[r] = znn;
               S.y[r] = yr + aP * dyr;
               S.vl[r] = nvl; S.vu[r] = nvu;
               S.s[r] = sn; S.pR[r] = pn; S.nR[r] = nn;
               S.d[r] = dtr;
+              tho += t;
             }
           });
+          tho = wsum(tho);
+          V[22] = tho;
           S.mu = V[4];
           for (int i = S.lanef(); i < nw; i += WAVE) S.U[i] = S.Ut[i];
           if (S.lanef() <= N) {
@@ -3153,15 +3304,28 @@ __device__ __forceinline__ int solve_one(Solver<CAP>& S, const Params* __restric
 
     // ===== line search (BacktrackingLineSearch + FilterLSAcceptor)
     double theta_ref = 0.0, gbd = 0.0, tiny_mx = 0.0, tiny_msv = 0.0;
+    // primal / dual fraction to the boundary of the step (dU, ds) at the current iterate,
+    // formed with the step's row pass; valid until the watchdog restores another iterate
+    double ftb_p = 1.0, ftb_d = 1.0;
+    bool ftb_ok = true;
     {
-      double th, g, msv, mx = 0.0;
-      S.row_step_ls(S.dX, mu, th, g, msv);
+      double th, g, msv, mx = 0.0, ap, ad;
+      S.row_step_ls(S.dX, mu, tau, th, g, msv, ap, ad);
       STAMP0();
       for (int i = S.lanef(); i < nw; i += WAVE) {
         const double du_ = S.dU[i];
         g += S.ru[i] * du_;
         mx = fmax(mx, fabs(du_ / (1.0 + fabs(S.U[i]))));
+        const double ui = S.U[i], xli = S.xl[i], xui = S.xu[i];
+        if (S.hasl(xli) && du_ < 0) ap = fmin(ap, (-tau * (ui - xli)) / du_);
+        if (S.hasu(xui) && -du_ < 0) ap = fmin(ap, (-tau * (xui - ui)) / (-du_));
+        double a1, a2;
+        S.dz_x(i, du_, a1, a2);
+        if (S.hasl(xli) && a1 < 0) ad = fmin(ad, (-tau * S.zl[i]) / a1);
+        if (S.hasu(xui) && a2 < 0) ad = fmin(ad, (-tau * S.zu[i]) / a2);
       }
+      ftb_p = wmin(ap);
+      ftb_d = wmin(ad);
       if (S.lanef() <= N) {
         double gx = 0.0;
 #pragma unroll
@@ -3239,6 +3403,7 @@ __device__ __forceinline__ int solve_one(Solver<CAP>& S, const Params* __restric
       theta_ref = WD[0]; phi_ref = WD[1]; gbd = WD[2];
       S.delta = WD[5];
       wd_dir = true;
+      ftb_ok = false;  // another iterate and step: the fused fractions no longer apply
       phic = false;
       in_wd = false;
       wd_cnt = 0;
@@ -3259,7 +3424,7 @@ __device__ __forceinline__ int solve_one(Solver<CAP>& S, const Params* __restric
         if (S.meq > 0)
           for (int r = S.lanef(); r < ng; r += WAVE) S.weqy_()[r] = S.eqy_()[r];
       }
-      const double at = S.frac_to_bound(tau, S.dU, S.ds);
+      const double at = ftb_ok ? ftb_p : S.frac_to_bound(tau, S.dU, S.ds);
       WD[0] = theta_ref; WD[1] = phi_ref; WD[2] = gbd; WD[3] = at; WD[4] = mu; WD[5] = S.delta;
       sync();
       in_wd = true;
@@ -3272,9 +3437,9 @@ __device__ __forceinline__ int solve_one(Solver<CAP>& S, const Params* __restric
     // soft restoration step (BacktrackingLineSearch::TrySoftRestoStep); returns
     // 0 rejected, 1 accepted, 2 accepted & satisfies the original criterion
     auto try_soft = [&]() -> int {
-      const double ap = S.frac_to_bound(tau, S.dU, S.ds);
+      const double ap = ftb_ok ? ftb_p : S.frac_to_bound(tau, S.dU, S.ds);
       S.mu = dir_mu();  // dual components of the step (its own mu); the barrier terms use mu
-      const double ad = S.dual_frac_to_bound(tau, S.dU, S.ds);
+      const double ad = (ftb_ok && !wd_dir) ? ftb_d : S.dual_frac_to_bound(tau, S.dU, S.ds);
       S.mu = mu;
       const double a = fmin(ap, ad);
       // current pd error (grad_lag from the adjoint computed at loop start)
@@ -3349,7 +3514,7 @@ __device__ __forceinline__ int solve_one(Solver<CAP>& S, const Params* __restric
       }
     } else {
       if (tiny) {
-        const double a = S.frac_to_bound(tau, S.dU, S.ds);
+        const double a = ftb_ok ? ftb_p : S.frac_to_bound(tau, S.dU, S.ds);
         double ft, phit, tht;
         ++ls_trials;
         if (S.trial(a, S.dU, S.ds, ft, phit, tht)) {
@@ -3362,7 +3527,7 @@ __device__ __forceinline__ int solve_one(Solver<CAP>& S, const Params* __restric
         if (in_wd) {
           // one trial at the full step, judged against the stored reference values with
           // the stored alpha test, no SOC (BacktrackingLineSearch::DoBacktrackingLineSearch)
-          const double amax_w = S.frac_to_bound(tau, S.dU, S.ds);
+          const double amax_w = ftb_ok ? ftb_p : S.frac_to_bound(tau, S.dU, S.ds);
           double ft, phit, tht;
           ++ls_trials;
           const bool okev = S.trial(amax_w, S.dU, S.ds, ft, phit, tht);
@@ -3388,7 +3553,7 @@ __device__ __forceinline__ int solve_one(Solver<CAP>& S, const Params* __restric
             amin = fmin(amin, o.delta * pow(theta_ref, o.s_theta) / pow(-gbd, o.s_phi));
         }
         amin *= o.alpha_min_frac;
-        const double amax_p = S.frac_to_bound(tau, S.dU, S.ds);
+        const double amax_p = ftb_ok ? ftb_p : S.frac_to_bound(tau, S.dU, S.ds);
         double a = skip_first ? amax_p * o.alpha_red_factor : amax_p;
         int n_steps = 0;
         while (a > amin || n_steps == 0) {
@@ -3423,8 +3588,7 @@ __device__ __forceinline__ int solve_one(Solver<CAP>& S, const Params* __restric
                 S.forward(S.dU2, S.dX);   // dX is free once gBD is known
                 S.refine(S.sigx, S.ru, S.dU2, S.dX);
               }
-              S.row_step(S.dX, S.dms, true, S.ds2);
-              a_soc = S.frac_to_bound(tau, S.dU2, S.ds2);
+              a_soc = S.row_step_soc(S.dX, S.dU2, S.ds2, tau);
               dsp = S.ds2;
               double ft2, phit2, tht2;
               ++ls_trials;
@@ -3485,7 +3649,8 @@ __device__ __forceinline__ int solve_one(Solver<CAP>& S, const Params* __restric
       const GLB double* dUa = (acc_kind == 2) ? S.dU2 : S.dU;
       const auto* dsa = (acc_kind == 2) ? S.ds2 : S.ds;
       S.mu = dir_mu();  // the step's dual components (mu below: the kappa_sigma safeguard)
-      if (acc_kind != 3) alpha_d = S.dual_frac_to_bound(tau, dUa, dsa);
+      if (acc_kind == 1 && ftb_ok && !wd_dir) alpha_d = ftb_d;  // the step's row pass formed it
+      else if (acc_kind != 3) alpha_d = S.dual_frac_to_bound(tau, dUa, dsa);
       const double ap = alpha_p, ad = alpha_d;
       const double ks = o.kappa_sigma;
       // bound multipliers of U (old slacks for the step, new slacks for kappa_sigma)
@@ -3833,7 +3998,6 @@ struct SchedQ {
   int one_set;  // test hook (NMPC_SCHED_TEST_ONE_SET): only the waves on XCD 0 run, so
                 // sets 1..7 are never drained and the check must report it
   int hot_iters;  // a step after one with >= hot_iters iterations goes to the hot family (0: none)
-  int hot_prio;   // 1: a wave runs a step claimed from the hot family at raised issue priority
 };
 constexpr unsigned long long kSchedWaitTicks = 1000000000ull;  // s_memrealtime (100 MHz): 10 s
 
@@ -3870,7 +4034,7 @@ __global__ __launch_bounds__(WAVE, CAP::wpe) void nmpc_closed_loop_sched_kernel(
   const long long ro = fo * q.BX;  // ring offset of the hot family
   int jmin = 0;
   for (;;) {
-    int cb = -1, ck = -1, cf = 0;
+    int cb = -1, ck = -1;
     if (threadIdx.x == 0) {
       // Hot queues first, then normal ones, each lowest step first.  Finding nothing to
       // claim means every unfinished scenario of the set is running on some wave, so
@@ -3902,7 +4066,7 @@ __global__ __launch_bounds__(WAVE, CAP::wpe) void nmpc_closed_loop_sched_kernel(
             v = ld_acq(rg + (long long)j * q.BX + h);
           }
           if (v < 0) __hip_atomic_store(q.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          else { cb = v; ck = j; cf = f; }
+          else { cb = v; ck = j; }
           claimed = true;
           break;
         }
@@ -3910,15 +4074,7 @@ __global__ __launch_bounds__(WAVE, CAP::wpe) void nmpc_closed_loop_sched_kernel(
     }
     cb = __builtin_amdgcn_readfirstlane(cb);
     ck = __builtin_amdgcn_readfirstlane(ck);
-    cf = __builtin_amdgcn_readfirstlane(cf);
     if (ck < 0) break;
-    // a hot step (its predecessor ran long: restoration / max_iter) is likely on the chain
-    // that bounds the launch; its wave takes precedence over the CU's other waves at the
-    // issue ports they share (LDS, vector memory, scalar), which do not change results
-    if (q.hot_prio) {
-      if (cf) __builtin_amdgcn_s_setprio(2);
-      else __builtin_amdgcn_s_setprio(0);
-    }
     int its = 0;
     if (cb >= 0 && cb < B) {  // an out-of-range dispatch entry is claimed and skipped
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // the previous step's p, w (L1 invalidated)
@@ -4641,8 +4797,6 @@ int nmpc_closed_loop_dev(nmpc_handle* h, int32_t B, int32_t K, const double* lbx
     // hot family threshold: half of max_iter (NMPC_SCHED_HOT overrides; 0 = one family only)
     q.hot_iters = h->hp.o.max_iter / 2 > 0 ? h->hp.o.max_iter / 2 : 1;
     if (const char* hv = std::getenv("NMPC_SCHED_HOT")) q.hot_iters = std::atoi(hv);
-    q.hot_prio = 1;
-    if (const char* hp = std::getenv("NMPC_SCHED_PRIO")) q.hot_prio = std::atoi(hp) != 0;
     const char* one = std::getenv("NMPC_SCHED_TEST_ONE_SET");
     q.one_set = (one && std::atoi(one) != 0) ? 1 : 0;
     const long long n = (long long)NXCD * K * BX;

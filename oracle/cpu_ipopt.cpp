@@ -755,7 +755,7 @@ class Solver {
   // The row keeps its slot with the slack pinned at the scaled target and no bounds; the
   // Newton step adds the rows through the Schur complement S = J_c H^-1 J_c^T of the
   // augmented system, from one unit solve per row with the Riccati factors.
-  static constexpr int MEQ = 16;  // the kernel's NMPC_MEQ
+  static constexpr int MEQ = 128;  // the kernel's NMPC_MEQ
   Mask eqm;
   int neq = 0;
   std::vector<int> eqi;

@@ -14,7 +14,7 @@ the fixture's solver by rounding alone:
 
 Two measurements per run, written to ref_run_<name>_spread.npz:
 
-  per step  (numpy1..3) each step's (w, p) of the fixture solved again: status,
+  per step  (numpy1..3, cpp) each step's (w, p) of the fixture solved again: status,
             iterations, and the largest relative deviation of x and f from the fixture.
             A step whose result moves under these rounding-level changes is a step at
             which the fixture's own x / iteration count is not determined beyond rounding
@@ -29,6 +29,8 @@ Two measurements per run, written to ref_run_<name>_spread.npz:
             their whole-run sums spread is the yardstick the GPU's loop is held to.
 
     python tests/golden/gen_rounding_spread.py [<run>|all] [--jobs 8]
+    python tests/golden/gen_rounding_spread.py --add-cpp-steps [<run>|all]
+        (adds the compiled restatement's per-step row to existing spread files)
 """
 import argparse
 import multiprocessing as mp
@@ -84,6 +86,38 @@ def per_step_job(args):
     return name, v, out
 
 
+def cpp_steps(name):
+    """Every fixture step re-solved by the compiled restatement (the Riccati Newton step:
+    the same algorithm, another factorisation of the same matrices): status, iterations,
+    relative deviation of x and f from the fixture."""
+    from oracle import nmpc_oracle as orc, cpu_ipopt
+    z = _fixture(name)
+    W = warm_starts(name, z)
+    c = cpu_ipopt.solve_batch(grr.run_problem(name), W, z["p"], z["lbx"], z["ubx"], z["lbg"], z["ubg"],
+                              orc.REFERENCE_OPTS, threads=8)
+    dx = np.max(np.abs(c["x"] - z["x"]) / (1 + np.abs(z["x"])), axis=1)
+    df = np.abs(c["f"] - z["f"]) / (1 + np.abs(z["f"]))
+    return c["status"].astype(np.int16), c["iter"].astype(np.int16), dx, df
+
+
+def add_cpp_steps(names):
+    for n in names:
+        path = os.path.join(HERE, f"ref_run_{n}_spread.npz")
+        sp = dict(np.load(path))
+        st, it, dx, df = cpp_steps(n)
+        k = len(VARIANTS)
+        sp["step_status"] = np.vstack([sp["step_status"][:k], st[None]])
+        sp["step_iter"] = np.vstack([sp["step_iter"][:k], it[None]])
+        sp["step_dev_x"] = np.vstack([sp["step_dev_x"][:k], dx[None]])
+        sp["step_dev_f"] = np.vstack([sp["step_dev_f"][:k], df[None]])
+        sp["step_solvers"] = np.array([f"numpy{v}" for v in VARIANTS] + ["cpp"])
+        np.savez_compressed(path, **sp)
+        z = _fixture(n)
+        conv = np.isin(z["status"], (0, 1))
+        print(f"{n}: cpp per step vs fixture: status {int((st != z['status']).sum())}, iter "
+              f"{int((it != z['iter']).sum())}, conv x>1e-6 {int((conv & (st == z['status']) & (dx > 1e-6)).sum())}")
+
+
 def whole_job(args):
     name, solver = args
     z = _fixture(name)
@@ -98,8 +132,12 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("run", nargs="?", default="all")
     ap.add_argument("--jobs", type=int, default=8)
+    ap.add_argument("--add-cpp-steps", action="store_true")
     a = ap.parse_args()
     names = list(grr.RUNS) if a.run == "all" else [a.run]
+    if a.add_cpp_steps:
+        add_cpp_steps(names)
+        return
     jobs_w = [(n, s) for n in names for s in WHOLE]
     jobs_w.sort(key=lambda j: -grr.RUNS[j[0]]["K"] * (0.05 if j[1] == "cpp" else 1.0))
     jobs_s = []
@@ -126,7 +164,11 @@ def main():
         for i, v in enumerate(VARIANTS):
             for k, s_, n_, x_, f_ in res_s[n][v]:
                 st[i, k], it[i, k], dx[i, k], df[i, k] = s_, n_, x_, f_
-        out = dict(step_variants=np.array(VARIANTS), step_status=st, step_iter=it, step_dev_x=dx, step_dev_f=df,
+        cst, cit, cdx, cdf = cpp_steps(n)
+        st, it = np.vstack([st, cst[None]]), np.vstack([it, cit[None]])
+        dx, df = np.vstack([dx, cdx[None]]), np.vstack([df, cdf[None]])
+        out = dict(step_variants=np.array(VARIANTS), step_solvers=np.array([f"numpy{v}" for v in VARIANTS] + ["cpp"]),
+                   step_status=st, step_iter=it, step_dev_x=dx, step_dev_f=df,
                    run_solvers=np.array(WHOLE), run_part=np.array([res_w[n][s]["part"] for s in WHOLE]),
                    run_fov_sum=np.array([res_w[n][s]["fov_sum"] for s in WHOLE]),
                    run_status=np.stack([res_w[n][s]["status"] for s in WHOLE]),

@@ -174,15 +174,24 @@ def test_reference_bounds_at_n_not_15_iterate_like_the_oracle(cpu, N):
     assert _relerr(r["x"][0], ref["x"]) <= TOL
 
 
-def test_too_many_equality_rows_is_invalid(cpu):
-    # more than 16 equality rows (the kernel's NMPC_MEQ): Invalid_Problem_Definition, as the kernel
+@pytest.mark.parametrize("N,n_eq", [(20, 40), (25, 80), (32, 136)])
+def test_many_equality_rows(cpu, N, n_eq):
+    """The reference's literal bound vectors at N != 15 (F3): every row past index 128 is
+    lbg = ubg = 0.  Up to 128 equality rows (the kernel's NMPC_MEQ) are solved -- the NLP is
+    infeasible and rank-deficient, so the run ends in restoration or at max_iter, never at
+    -11; more report Invalid_Problem_Definition (-11), as the kernel."""
     from oracle import nmpc_oracle as orc
     from tests.test_oracle import reference_bounds_literal
-    lbx, ubx, lbg, ubg = reference_bounds_literal(20)  # 40 equality rows
-    prob = orc.make_problem("nmpc_tt", N=20, T=1.0)
+    lbx, ubx, lbg, ubg = reference_bounds_literal(N)
+    assert int(np.sum(lbg == ubg)) == n_eq
+    prob = orc.make_problem("nmpc_tt", N=N, T=1.0)
     p = np.array([90, 150, 80, 0, 0, 0, 0, 0, 100, 150, 0.0])
     r = cpu.solve_batch(prob, np.zeros((1, prob.nw)), p[None], lbx, ubx, lbg, ubg, orc.REFERENCE_OPTS)
-    assert r["status"][0] == -11
+    if n_eq > 128:
+        assert r["status"][0] == -11
+    else:
+        assert r["status"][0] in (orc.MAXIMUM_ITERATIONS_EXCEEDED, orc.INFEASIBLE_PROBLEM_DETECTED)
+        assert np.all(np.isfinite(r["x"][0]))
 
 
 @pytest.mark.parametrize("model", ["uav8g", "uav5"])

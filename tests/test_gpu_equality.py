@@ -46,8 +46,10 @@ def test_pinned_height_matches_oracle(b):
     assert _rel(sol["lam_g"].ravel()[row], ref["lam_g"][row]) <= 1e-5
 
 
-@pytest.mark.parametrize("N", [16, 17])
+@pytest.mark.parametrize("N", [16, 17, 20, 25])
 def test_reference_bounds_at_n_not_15_match_oracle(N):
+    """8, 16, 40 and 80 equality rows: the Schur step holds up to 128 (lane l owns rows l and
+    l + 64 of S), so the kernel returns the oracle's status, not -11."""
     lbx, ubx, lbg, ubg = reference_bounds_literal(N)
     prob = orc.make_problem("nmpc_tt", N=N, T=1.0)
     p = np.array([90, 150, 80, 0, 0, 0, 0, 0, 100, 150, 0.0])  # Python/NMPC_TT.py:57-58,316-339
@@ -61,12 +63,12 @@ def test_reference_bounds_at_n_not_15_match_oracle(N):
         assert _rel(sol["x"].ravel(), ref["x"]) <= TOL
 
 
-def test_too_many_equality_rows_is_invalid_problem():
-    # more than NMPC_MEQ (16) equality rows: Invalid_Problem_Definition (-11), documented
-    lbx, ubx, lbg, ubg = reference_bounds_literal(20)  # 40 equality rows
-    prob = orc.make_problem("nmpc_tt", N=20, T=1.0)
+def test_more_than_128_equality_rows_is_invalid_problem():
+    # more than NMPC_MEQ (128) equality rows: Invalid_Problem_Definition (-11), documented
+    lbx, ubx, lbg, ubg = reference_bounds_literal(32)  # 136 equality rows
+    prob = orc.make_problem("nmpc_tt", N=32, T=1.0)
     p = np.array([90, 150, 80, 0, 0, 0, 0, 0, 100, 150, 0.0])
-    _, st = _gpu_solve("nmpc_tt", 20, 1.0, np.zeros(prob.nw), lbx, ubx, lbg, ubg, p)
+    _, st = _gpu_solve("nmpc_tt", 32, 1.0, np.zeros(prob.nw), lbx, ubx, lbg, ubg, p)
     assert int(np.ravel(st["status_code"])[0]) == -11
 
 
@@ -192,7 +194,8 @@ def test_watchdog_stop_with_equality_rows_matches_oracle(case, last, skip):
     ipo = orc.IpoptDense(prob, orc.REFERENCE_OPTS)
     ref = ipo.solve(np.zeros(prob.nw), lbx, ubx, lbg, ubg, p, trace=True)
     stops = [i for i in ipo.wd_stop_its if i <= last]
-    assert stops and all(i > skip for i in stops[:1]), ipo.wd_stop_its  # the window exercises StopWatchDog
+    # the window exercises StopWatchDog, and the left-out trial iteration is the one it discards
+    assert stops and (skip + 1) in ipo.wd_stop_its, ipo.wd_stop_its
     from nmpc_amd import nlpsol, make_spec, REFERENCE_OPTS
     s = nlpsol("solver", "ipopt", make_spec("race_track_2", N=8, T=0.2), REFERENCE_OPTS)
     s.set_trace(True)
