@@ -197,6 +197,17 @@ struct Cap {
   // row passes: trips of 64 rows processed together (their loads batched), <= 5
   static constexpr int rtrips = (MMAX * (NMAX + 1) + 63) / 64;
   static constexpr int ru = rtrips < 2 ? rtrips : 2;
+  // deep: register-hungry latency hiding (control passes two trips at a time, gains
+  // fetched three stages ahead in the forward sweep, stored factors one stage ahead in the
+  // re-solve) -- for the one-wave-per-SIMD LDS class; the global-row classes, held to half
+  // the registers, spill with it and lose (config 5 measured)
+#ifndef NMPC_DEEP_GLOBAL
+#define NMPC_DEEP_GLOBAL 0
+#endif
+  static constexpr bool deep = LDSR || NMPC_DEEP_GLOBAL;
+  // control passes: trips of 64 decision variables processed together, <= 2
+  static constexpr int ctrips = (6 * NMAX + 63) / 64;
+  static constexpr int cu = !deep ? 1 : (ctrips < 2 ? ctrips : 2);
 };
 
 struct IO {
@@ -366,6 +377,20 @@ struct Solver {
         const int r = base + u * WAVE + lanef();
         const bool on = r < ng;
         f(on ? r : ng - 1, on);
+      }
+    }
+  }
+  // the same for the decision variables (index clamped to the last one when off: every
+  // load is valid, so a pass's loads over its trips issue together; f guards its sums and
+  // stores with `on`)
+  template <class F>
+  __device__ __forceinline__ void ctrls(F&& f) const {
+    for (int base = 0; base < nw; base += CAP::cu * WAVE) {
+#pragma unroll
+      for (int u = 0; u < CAP::cu; ++u) {
+        const int i = base + u * WAVE + lanef();
+        const bool on = i < nw;
+        f(on ? i : nw - 1, on);
       }
     }
   }
@@ -785,16 +810,20 @@ struct Solver {
   // iteration's reference value (same slacks bit for bit: U <- Ut, s <- s + a ds)
   // per-lane partial sums: the control terms first, then the rows in rows() order
   __device__ __forceinline__ void barrier_ctrl(const GLB double* u, double& logs, double& damp) const {
-    for (int i = lanef(); i < nw; i += WAVE) barrier_ctrl1(i, u[i], logs, damp);
+    ctrls([&](int i, bool on) { barrier_ctrl1(i, on, u[i], logs, damp); });
   }
   // one control's barrier terms at the value ui (a register: the trial point's controls
   // are formed and consumed in the same pass, no store -> load round trip)
-  __device__ __forceinline__ void barrier_ctrl1(int i, double ui, double& logs, double& damp) const {
-    const bool lo = hasl(xl[i]), hi = hasu(xu[i]);
-    if (lo) logs += log(ui - xl[i]);
-    if (hi) logs += log(xu[i] - ui);
-    if (lo && !hi) damp += ui - xl[i];
-    if (hi && !lo) damp += xu[i] - ui;
+  __device__ __forceinline__ void barrier_ctrl1(int i, bool on, double ui, double& logs, double& damp) const {
+    const double xli = xl[i], xui = xu[i];
+    const bool lo = hasl(xli), hi = hasu(xui);
+    const double ll = log(ui - xli), lu = log(xui - ui);
+    if (on) {
+      if (lo) logs += ll;
+      if (hi) logs += lu;
+      if (lo && !hi) damp += ui - xli;
+      if (hi && !lo) damp += xui - ui;
+    }
   }
   __device__ __forceinline__ void barrier_row(int r, bool on, double sv, double& logs, double& damp) const {
     const double lo_ = dl[r], hi_ = du[r];
@@ -1187,6 +1216,7 @@ struct Solver {
     //     solve; dt: trial constraints, rewritten by the next trial)
     auto Wr = ds2;
     auto Br = dt;
+    const bool curv = !(mode == SUM_LS || mode == SUM_LS_RESTO);  // y-weighted row curvature
     rows([&](int r, bool on) {
       const double dcr = dc[r];
       double A, Bw;
@@ -1232,7 +1262,6 @@ struct Solver {
       const LDS double* xk = X + k * 8;
       double Qxy0 = 0, Qxy1 = 0, Qxy2 = 0, qx = 0, qy = 0;
       double Qb[5] = {0, 0, 0, 0, 0}, qb[5] = {0, 0, 0, 0, 0};
-      const bool curv = !(mode == SUM_LS || mode == SUM_LS_RESTO);  // y-weighted row curvature
       for (int i = 0; i < m; ++i) {
         const int r = k * m + i;
         const double w = soc ? 0.0 : Wr[r], bw = Br[r];
@@ -1573,14 +1602,15 @@ struct Solver {
     R p8[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) p8[i] = ZQ ? (R)0 : (R)qs[N * 10 + i];
-    for (int k = N - 1; k >= 0; --k) {
+    // one stage of the backward recursion with its stored R~_k (Lin) and r_k (rin)
+    auto stage = [&](int k, const R (&Lin)[21], const R (&rin)[6]) {
       double E03d, E04d, E13d, E14d, E23d, b00d, b10d, b20d;
       stage_AB(k, E03d, E04d, E13d, E14d, E23d, b00d, b10d, b20d);
       const R E03 = (R)E03d, E04 = (R)E04d, E13 = (R)E13d, E14 = (R)E14d, E23 = (R)E23d;
       const R b00 = (R)b00d, b10 = (R)b10d, b20 = (R)b20d, Tr = (R)T;
       R Lm[21], idg[6], rt[6], v[6];
 #pragma unroll
-      for (int t = 0; t < 21; ++t) Lm[t] = (R)Rk[k * 21 + t];
+      for (int t = 0; t < 21; ++t) Lm[t] = Lin[t];
 #pragma unroll
       for (int c = 0; c < 6; ++c) {
         R dg = Lm[c * (c + 1) / 2 + c];
@@ -1597,9 +1627,9 @@ struct Solver {
           Lm[r * (r + 1) / 2 + c] = a * ig;
         }
       }
-      rt[0] = (R)rv[k * 6 + 0] + ((b00 * p8[0] + b10 * p8[1]) + b20 * p8[2]);
+      rt[0] = rin[0] + ((b00 * p8[0] + b10 * p8[1]) + b20 * p8[2]);
 #pragma unroll
-      for (int r = 1; r < 6; ++r) rt[r] = (R)rv[k * 6 + r] + Tr * p8[2 + r];
+      for (int r = 1; r < 6; ++r) rt[r] = rin[r] + Tr * p8[2 + r];
       if (nfix > 0) {
         const int fm = fixm[k];
 #pragma unroll
@@ -1637,6 +1667,32 @@ struct Solver {
       }
 #pragma unroll
       for (int i = 0; i < 8; ++i) p8[i] = pn[i];
+    };
+    // the stored R~_k and r_k do not depend on the recursion: stage k-1's are fetched while
+    // stage k is formed (two stages per trip, alternating register sets; clamped fetches)
+    R LA[21], LB[21], rA[6], rB[6];
+    auto fetch = [&](R (&Lo)[21], R (&ro)[6], int ks) {
+      const int kc = ks > 0 ? ks : 0;
+#pragma unroll
+      for (int t = 0; t < 21; ++t) Lo[t] = (R)Rk[kc * 21 + t];
+#pragma unroll
+      for (int r = 0; r < 6; ++r) ro[r] = (R)rv[kc * 6 + r];
+    };
+    if constexpr (CAP::deep) {
+      fetch(LA, rA, N - 1);
+      for (int k = N - 1; k >= 0; k -= 2) {
+        fetch(LB, rB, k - 1);
+        stage(k, LA, rA);
+        if (k == 0) break;
+        fetch(LA, rA, k - 2);
+        stage(k - 1, LB, rB);
+      }
+    } else {
+      (void)LB; (void)rB;
+      for (int k = N - 1; k >= 0; --k) {
+        fetch(LA, rA, k);
+        stage(k, LA, rA);
+      }
     }
     sync();
     STAMP1(PH_RESOLVE);
@@ -1756,30 +1812,45 @@ struct Solver {
 #pragma unroll
       for (int c = 0; c < 8; ++c) dx[c] = xn[c];
     };
-    // K_k rows come from global memory and do not depend on dx: stage k+1's row is
-    // fetched while stage k is formed, into the other of two register sets (two stages
-    // per trip, so no register copies between stages)
-    double KA[8], KB[8], kA, kB;
-#pragma unroll
-    for (int c = 0; c < 8; ++c) KA[c] = K[r * 8 + c];
-    kA = kf[r];
+    // K_k rows come from global memory and do not depend on dx: they are fetched ahead,
+    // into register sets used in turn (no register copies between stages).  A stage's
+    // arithmetic is far shorter than a global load's latency, so the deep classes fetch
+    // three stages ahead (four sets), the others one (two sets).
+    double K0[8], K1[8], K2[8], K3[8], k0, k1, k2, k3;
     // (fetches clamped to the last stage rather than guarded: no branch, see riccati_)
-    for (int k = 0; k < N; k += 2) {
-      {
-        const int kb = k + 1 < N ? k + 1 : N - 1;
+    auto fetch = [&](double (&Kr)[8], double& kk, int ks) {
+      const int kc = ks < N ? ks : N - 1;
 #pragma unroll
-        for (int c = 0; c < 8; ++c) KB[c] = K[kb * 48 + r * 8 + c];
-        kB = kf[kb * 6 + r];
+      for (int c = 0; c < 8; ++c) Kr[c] = K[kc * 48 + r * 8 + c];
+      kk = kf[kc * 6 + r];
+    };
+    if constexpr (CAP::deep) {
+      fetch(K0, k0, 0);
+      fetch(K1, k1, 1);
+      fetch(K2, k2, 2);
+      for (int k = 0; k < N; k += 4) {
+        fetch(K3, k3, k + 3);
+        stage(k, K0, k0);
+        if (k + 1 >= N) break;
+        fetch(K0, k0, k + 4);
+        stage(k + 1, K1, k1);
+        if (k + 2 >= N) break;
+        fetch(K1, k1, k + 5);
+        stage(k + 2, K2, k2);
+        if (k + 3 >= N) break;
+        fetch(K2, k2, k + 6);
+        stage(k + 3, K3, k3);
       }
-      stage(k, KA, kA);
-      if (k + 1 >= N) break;
-      {
-        const int ka = k + 2 < N ? k + 2 : N - 1;
-#pragma unroll
-        for (int c = 0; c < 8; ++c) KA[c] = K[ka * 48 + r * 8 + c];
-        kA = kf[ka * 6 + r];
+    } else {
+      (void)K2; (void)K3; (void)k2; (void)k3;
+      fetch(K0, k0, 0);
+      for (int k = 0; k < N; k += 2) {
+        fetch(K1, k1, k + 1);
+        stage(k, K0, k0);
+        if (k + 1 >= N) break;
+        fetch(K0, k0, k + 2);
+        stage(k + 1, K1, k1);
       }
-      stage(k + 1, KB, kB);
     }
     sync();
     STAMP1(PH_FWD);
@@ -2003,13 +2074,14 @@ struct Solver {
     // the trial controls, their barrier terms and the proximity term in one pass (each
     // accumulator keeps the per-lane order of barrier_obj / resto_pn_terms)
     double th = 0.0, logs = 0.0, damp = 0.0, pn = 0.0, lg = 0.0, prox = 0.0;
-    for (int i = lanef(); i < nw; i += WAVE) {
+    ctrls([&](int i, bool on) {
       const double ui = U[i] + a * dUs[i];
-      Ut[i] = ui;
-      barrier_ctrl1(i, ui, logs, damp);
+      if (on) Ut[i] = ui;
+      barrier_ctrl1(i, on, ui, logs, damp);
       const double dd = ui - UR[i];
-      prox += dr2(i) * dd * dd;
-    }
+      const double pv = dr2(i) * dd * dd;
+      if (on) prox += pv;
+    });
     sync();
     rollout(U, Xt, dUs, a);
     fo = df * eval_fg(Xt, dt, dc);
@@ -2070,11 +2142,11 @@ struct Solver {
                                                     F&& extra) const {
     STAMP0();
     double a = 1.0;
-    for (int i = lanef(); i < nw; i += WAVE) {
+    ctrls([&](int i, bool on) {  // (a repeated last entry leaves a minimum unchanged)
       const double dx = dUs[i];
       if (hasl(xl[i]) && dx < 0) a = fmin(a, (-tau_ * (U[i] - xl[i])) / dx);
       if (hasu(xu[i]) && -dx < 0) a = fmin(a, (-tau_ * (xu[i] - U[i])) / (-dx));
-    }
+    });
     rows([&](int r, bool on) {
       const double dd = dss[r], sr = s[r], lo = dl[r], hi = du[r];
       const double al = (-tau_ * (sr - lo)) / dd, au = (-tau_ * (hi - sr)) / (-dd);
@@ -2106,12 +2178,12 @@ struct Solver {
                                                          F&& extra) const {
     STAMP0();
     double a = 1.0;
-    for (int i = lanef(); i < nw; i += WAVE) {
+    ctrls([&](int i, bool on) {
       double a1, a2;
       dz_x(i, dUs[i], a1, a2);
       if (hasl(xl[i]) && a1 < 0) a = fmin(a, (-tau_ * zl[i]) / a1);
       if (hasu(xu[i]) && a2 < 0) a = fmin(a, (-tau_ * zu[i]) / a2);
-    }
+    });
     rows([&](int r, bool on) {
       const double sr = s[r], lo = dl[r], hi = du[r], vlr = vl[r], vur = vu[r], dsv = dss[r];
       const bool hl = hasl(lo), hu = hasu(hi);
@@ -2140,10 +2212,10 @@ struct Solver {
   // complementarity max |S z - mu_| over all bounds
   __device__ __forceinline__ double compl_max(double mu_) const {
     double c = 0.0;
-    for (int i = lanef(); i < nw; i += WAVE) {
+    ctrls([&](int i, bool on) {
       if (hasl(xl[i])) c = fmax(c, fabs((U[i] - xl[i]) * zl[i] - mu_));
       if (hasu(xu[i])) c = fmax(c, fabs((xu[i] - U[i]) * zu[i] - mu_));
-    }
+    });
     rows([&](int r, bool on) {
       const double sr = s[r], lo = dl[r], hi = du[r], vlr = vl[r], vur = vu[r];
       const double cl = fabs((sr - lo) * vlr - mu_), cu = fabs((hi - sr) * vur - mu_);
@@ -2208,11 +2280,11 @@ struct Solver {
                         double& tht) {
     // the trial controls and their barrier terms in one pass
     double th = 0.0, logs = 0.0, damp = 0.0;
-    for (int i = lanef(); i < nw; i += WAVE) {
+    ctrls([&](int i, bool on) {
       const double ui = U[i] + a * dUs[i];
-      Ut[i] = ui;
-      barrier_ctrl1(i, ui, logs, damp);
-    }
+      if (on) Ut[i] = ui;
+      barrier_ctrl1(i, on, ui, logs, damp);
+    });
     sync();
     rollout(U, Xt, dUs, a);
     ft = df * eval_fg(Xt, dt, dc);
@@ -2388,7 +2460,7 @@ __device__ __forceinline__ void resto_phase(const Params* __restrict__ prm, doub
         double cmu = 0, pinfu = 0;
         const double muc = V[4];
         bool bad = false;
-        for (int i = S.lanef(); i < nw; i += WAVE) {
+        S.ctrls([&](int i, bool on) {  // (maxima and flags ignore the repeated last entry)
           const double dd = S.U[i] - S.UR[i];
           const double g = S.fixed(i) ? 0.0 : S.grad_u(i) + S.etaR * S.dr2(i) * dd - S.zl[i] + S.zu[i];
           if (!isfinite(g)) bad = true;
@@ -2397,9 +2469,9 @@ __device__ __forceinline__ void resto_phase(const Params* __restrict__ prm, doub
           if (S.hasu(S.xu[i])) cmr = fmax(cmr, fabs((S.xu[i] - S.U[i]) * S.zu[i]));
           if (S.hasl(S.xl[i])) cmu = fmax(cmu, fabs((S.U[i] - S.xl[i]) * S.zl[i] - muc));
           if (S.hasu(S.xu[i])) cmu = fmax(cmu, fabs((S.xu[i] - S.U[i]) * S.zu[i] - muc));
-          sumz += fabs(S.zl[i]) + fabs(S.zu[i]);
-          frx += S.dr2(i) * dd * dd;
-        }
+          const double sz = fabs(S.zl[i]) + fabs(S.zu[i]), fx = S.dr2(i) * dd * dd;
+          if (on) { sumz += sz; frx += fx; }
+        });
         S.rows([&](int r, bool on) {
           const double yr = S.y[r], pr = S.pR[r], nr = S.nR[r], vlr = S.vl[r], vur = S.vu[r];
           const double zp = S.zpR[r], zn = S.znR[r], dr = S.d[r], sr = S.s[r], dcr = S.dc[r];
@@ -2504,14 +2576,16 @@ __device__ __forceinline__ void resto_phase(const Params* __restrict__ prm, doub
         STAMP1(PH_CONV);
         // ---- Newton step of the restoration problem (p, n eliminated per row)
         { STAMP0();
-        for (int i = S.lanef(); i < nw; i += WAVE) {
+        const double muR4 = V[4];  // volatile LDS scalar read once
+        S.ctrls([&](int i, bool on) {
           const bool hl = S.hasl(S.xl[i]), hu = S.hasu(S.xu[i]);
           const double Sl = hl ? S.U[i] - S.xl[i] : 1.0, Su = hu ? S.xu[i] - S.U[i] : 1.0;
           const double w2 = S.etaR * S.dr2(i);
-          S.sigx[i] = w2 + ((hl ? S.zl[i] / Sl : 0.0) + (hu ? S.zu[i] / Su : 0.0));
-          S.ru[i] = w2 * (S.U[i] - S.UR[i]) + (-(hl ? V[4] / Sl : 0.0) + (hu ? V[4] / Su : 0.0) +
-                    kd * V[4] * ((hl && !hu ? 1.0 : 0.0) - (hu && !hl ? 1.0 : 0.0)));
-        }
+          const double sg = w2 + ((hl ? S.zl[i] / Sl : 0.0) + (hu ? S.zu[i] / Su : 0.0));
+          const double rr = w2 * (S.U[i] - S.UR[i]) + (-(hl ? muR4 / Sl : 0.0) + (hu ? muR4 / Su : 0.0) +
+                            kd * muR4 * ((hl && !hu ? 1.0 : 0.0) - (hu && !hl ? 1.0 : 0.0)));
+          if (on) { S.sigx[i] = sg; S.ru[i] = rr; }
+        });
         sync();
         STAMP1(PH_SIGX); }
         if (V[9] > 0) V[8] = V[9];
@@ -2542,9 +2616,10 @@ __device__ __forceinline__ void resto_phase(const Params* __restrict__ prm, doub
           double th, g, ap, ad;
           const double tauR = V[5];
           S.row_step_resto(S.dX, false, S.ds, S.dpR, S.dnR, S.dyR, th, g, tauR, ap, ad);
-          for (int i = S.lanef(); i < nw; i += WAVE) {
+          S.ctrls([&](int i, bool on) {
             const double du_ = S.dU[i];
-            g += S.ru[i] * du_;
+            const double gi = S.ru[i] * du_;
+            if (on) g += gi;
             const double ui = S.U[i], xli = S.xl[i], xui = S.xu[i];
             if (S.hasl(xli) && du_ < 0) ap = fmin(ap, (-tauR * (ui - xli)) / du_);
             if (S.hasu(xui) && -du_ < 0) ap = fmin(ap, (-tauR * (xui - ui)) / (-du_));
@@ -2552,7 +2627,7 @@ __device__ __forceinline__ void resto_phase(const Params* __restrict__ prm, doub
             S.dz_x(i, du_, a1, a2);
             if (S.hasl(xli) && a1 < 0) ad = fmin(ad, (-tauR * S.zl[i]) / a1);
             if (S.hasu(xui) && a2 < 0) ad = fmin(ad, (-tauR * S.zu[i]) / a2);
-          }
+          });
           V[15] = wsum(th);
           V[16] = wsum(g);
           rftb_p = wmin(ap);
@@ -2677,11 +2752,11 @@ __device__ __forceinline__ void resto_phase(const Params* __restrict__ prm, doub
               double ap, u1;
               const double tauR = V[5];
               S.row_step_resto(S.dX, true, S.ds2, S.dp2R, S.dn2R, S.dy2R, t0, t1, tauR, ap, u1);
-              for (int i = S.lanef(); i < nw; i += WAVE) {  // frac_to_bound_resto's control part
+              S.ctrls([&](int i, bool) {  // frac_to_bound_resto's control part
                 const double du_ = S.dU2[i], ui = S.U[i], xli = S.xl[i], xui = S.xu[i];
                 if (S.hasl(xli) && du_ < 0) ap = fmin(ap, (-tauR * (ui - xli)) / du_);
                 if (S.hasu(xui) && -du_ < 0) ap = fmin(ap, (-tauR * (xui - ui)) / (-du_));
-              }
+              });
               a_soc = wmin(ap);
               dsp = S.ds2; dpp = S.dp2R; dnp = S.dn2R;
               double fo2, ph2, th2;
@@ -2718,17 +2793,18 @@ __device__ __forceinline__ void resto_phase(const Params* __restrict__ prm, doub
           if (rwd_dir) S.mu = WD[4];
           const double ad = (acc == 1 && rftb_ok && !rwd_dir) ? rftb_d
                                                                : S.dual_frac_to_bound_resto(V[5], dUa, dsa, dpa, dna);
-          for (int i = S.lanef(); i < nw; i += WAVE) {
+          const double muA = V[4];  // volatile LDS scalar read once
+          S.ctrls([&](int i, bool on) {
             double dzl, dzu;
             S.dz_x(i, dUa[i], dzl, dzu);
             double nzl = S.zl[i] + ad * dzl, nzu = S.zu[i] + ad * dzu;
             const double un = S.Ut[i];
-            if (S.hasl(S.xl[i])) { const double Sn = un - S.xl[i]; nzl = fmax(fmin(nzl, ks * V[4] / Sn), V[4] / (ks * Sn)); }
+            if (S.hasl(S.xl[i])) { const double Sn = un - S.xl[i]; nzl = fmax(fmin(nzl, ks * muA / Sn), muA / (ks * Sn)); }
             else nzl = 0.0;
-            if (S.hasu(S.xu[i])) { const double Sn = S.xu[i] - un; nzu = fmax(fmin(nzu, ks * V[4] / Sn), V[4] / (ks * Sn)); }
+            if (S.hasu(S.xu[i])) { const double Sn = S.xu[i] - un; nzu = fmax(fmin(nzu, ks * muA / Sn), muA / (ks * Sn)); }
             else nzu = 0.0;
-            S.zl[i] = nzl; S.zu[i] = nzu;
-          }
+            if (on) { S.zl[i] = nzl; S.zu[i] = nzu; }
+          });
           const double muR = V[4], aP = V[19];  // volatile LDS scalars read once
           const double dmuR = rwd_dir ? (double)WD[4] : muR;
           double tho = 0.0;  // theta of the original problem at the new iterate (next check)
@@ -2765,7 +2841,10 @@ __device__ __forceinline__ void resto_phase(const Params* __restrict__ prm, doub
           tho = wsum(tho);
           V[22] = tho;
           S.mu = V[4];
-          for (int i = S.lanef(); i < nw; i += WAVE) S.U[i] = S.Ut[i];
+          S.ctrls([&](int i, bool on) {
+            const double ut = S.Ut[i];
+            if (on) S.U[i] = ut;
+          });
           if (S.lanef() <= N) {
 #pragma unroll
             for (int c = 0; c < 8; ++c) S.X[S.lanef() * 8 + c] = S.Xt[S.lanef() * 8 + c];
@@ -3158,7 +3237,7 @@ __device__ __forceinline__ int solve_one(Solver<CAP>& S, const Params* __restric
     double cmu = 0;  // = compl_max(mu) of the barrier update below, from the same pass
     const double muc = S.mu;
     bool bad = false;
-    for (int i = S.lanef(); i < nw; i += WAVE) {
+    S.ctrls([&](int i, bool on) {  // (maxima and flags ignore the repeated last entry)
       const double g = S.fixed(i) ? 0.0 : S.grad_u(i) - S.zl[i] + S.zu[i];
       if (!isfinite(g)) bad = true;
       dinf = fmax(dinf, fabs(g));
@@ -3166,8 +3245,9 @@ __device__ __forceinline__ int solve_one(Solver<CAP>& S, const Params* __restric
       if (S.hasu(S.xu[i])) cmp = fmax(cmp, fabs((S.xu[i] - S.U[i]) * S.zu[i]));
       if (S.hasl(S.xl[i])) cmu = fmax(cmu, fabs((S.U[i] - S.xl[i]) * S.zl[i] - muc));
       if (S.hasu(S.xu[i])) cmu = fmax(cmu, fabs((S.xu[i] - S.U[i]) * S.zu[i] - muc));
-      sumz += fabs(S.zl[i]) + fabs(S.zu[i]);
-    }
+      const double sz = fabs(S.zl[i]) + fabs(S.zu[i]);
+      if (on) sumz += sz;
+    });
     S.rows([&](int r, bool on) {
       const double yr = S.y[r], vlr = S.vl[r], vur = S.vu[r], dr = S.d[r], sr = S.s[r], dcr = S.dc[r];
       const double lo = S.dl[r], hi = S.du[r];
@@ -3258,13 +3338,14 @@ __device__ __forceinline__ int solve_one(Solver<CAP>& S, const Params* __restric
 
     // ===== search direction with inertia correction (PDPerturbationHandler)
     { STAMP0();
-    for (int i = S.lanef(); i < nw; i += WAVE) {
+    S.ctrls([&](int i, bool on) {
       const bool hl = S.hasl(S.xl[i]), hu = S.hasu(S.xu[i]);
       const double Sl = hl ? S.U[i] - S.xl[i] : 1.0, Su = hu ? S.xu[i] - S.U[i] : 1.0;
-      S.sigx[i] = (hl ? S.zl[i] / Sl : 0.0) + (hu ? S.zu[i] / Su : 0.0);
-      S.ru[i] = -(hl ? mu / Sl : 0.0) + (hu ? mu / Su : 0.0) +
-                o.kappa_d * mu * ((hl && !hu ? 1.0 : 0.0) - (hu && !hl ? 1.0 : 0.0));
-    }
+      const double sg = (hl ? S.zl[i] / Sl : 0.0) + (hu ? S.zu[i] / Su : 0.0);
+      const double rr = -(hl ? mu / Sl : 0.0) + (hu ? mu / Su : 0.0) +
+                        o.kappa_d * mu * ((hl && !hu ? 1.0 : 0.0) - (hu && !hl ? 1.0 : 0.0));
+      if (on) { S.sigx[i] = sg; S.ru[i] = rr; }
+    });
     sync();
     STAMP1(PH_SIGX); }
     if (MV[3] > 0) MV[2] = MV[3];
@@ -3312,9 +3393,10 @@ __device__ __forceinline__ int solve_one(Solver<CAP>& S, const Params* __restric
       double th, g, msv, mx = 0.0, ap, ad;
       S.row_step_ls(S.dX, mu, tau, th, g, msv, ap, ad);
       STAMP0();
-      for (int i = S.lanef(); i < nw; i += WAVE) {
+      S.ctrls([&](int i, bool on) {
         const double du_ = S.dU[i];
-        g += S.ru[i] * du_;
+        const double gi = S.ru[i] * du_;
+        if (on) g += gi;
         mx = fmax(mx, fabs(du_ / (1.0 + fabs(S.U[i]))));
         const double ui = S.U[i], xli = S.xl[i], xui = S.xu[i];
         if (S.hasl(xli) && du_ < 0) ap = fmin(ap, (-tau * (ui - xli)) / du_);
@@ -3323,7 +3405,7 @@ __device__ __forceinline__ int solve_one(Solver<CAP>& S, const Params* __restric
         S.dz_x(i, du_, a1, a2);
         if (S.hasl(xli) && a1 < 0) ad = fmin(ad, (-tau * S.zl[i]) / a1);
         if (S.hasu(xui) && a2 < 0) ad = fmin(ad, (-tau * S.zu[i]) / a2);
-      }
+      });
       ftb_p = wmin(ap);
       ftb_d = wmin(ad);
       if (S.lanef() <= N) {
@@ -3654,7 +3736,7 @@ __device__ __forceinline__ int solve_one(Solver<CAP>& S, const Params* __restric
       const double ap = alpha_p, ad = alpha_d;
       const double ks = o.kappa_sigma;
       // bound multipliers of U (old slacks for the step, new slacks for kappa_sigma)
-      for (int i = S.lanef(); i < nw; i += WAVE) {
+      S.ctrls([&](int i, bool on) {
         double dzl, dzu;
         S.dz_x(i, dUa[i], dzl, dzu);
         double nzl = S.zl[i] + ad * dzl, nzu = S.zu[i] + ad * dzu;
@@ -3663,8 +3745,8 @@ __device__ __forceinline__ int solve_one(Solver<CAP>& S, const Params* __restric
         else nzl = 0.0;
         if (S.hasu(S.xu[i])) { const double Sn = S.xu[i] - un; nzu = fmax(fmin(nzu, ks * mu / Sn), mu / (ks * Sn)); }
         else nzu = 0.0;
-        S.zl[i] = nzl; S.zu[i] = nzu;
-      }
+        if (on) { S.zl[i] = nzl; S.zu[i] = nzu; }
+      });
       const double kdm = o.kappa_d * S.mu, dlt = S.delta;
       S.rows([&](int r, bool on) {
         const double sr = S.s[r], yr = S.y[r], vlr = S.vl[r], vur = S.vu[r], dsr = dsa[r], dtr = S.dt[r];
@@ -3691,7 +3773,10 @@ __device__ __forceinline__ int solve_one(Solver<CAP>& S, const Params* __restric
         }
       });
       S.mu = mu;
-      for (int i = S.lanef(); i < nw; i += WAVE) S.U[i] = S.Ut[i];
+      S.ctrls([&](int i, bool on) {
+        const double ut = S.Ut[i];
+        if (on) S.U[i] = ut;
+      });
       if (S.lanef() <= N) {
 #pragma unroll
         for (int c = 0; c < 8; ++c) S.X[S.lanef() * 8 + c] = S.Xt[S.lanef() * 8 + c];
