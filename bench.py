@@ -112,15 +112,23 @@ def cpu_baseline(spec_cfg, cfg, P, lbx, ubx, lbg, ubg, K, W=0, p_step=None, budg
     except AttributeError:
         ncpu = os.cpu_count() or 1
     nthr = max(1, min(16, ncpu))  # the GPU box's CPU share is 16
-    layout = None if spec_cfg.n_obs == 0 else ("race_track_2" if spec_cfg.n_obs == 10 else "nmpc_tt")
-    prob = orc.make_problem(layout, N=spec_cfg.N, T=spec_cfg.T, model=spec_cfg.model)
-    # the W warm-up steps, untimed, for every scenario (the GPU runs them as W per-step launches)
+    # the oracle's description of the same problem (nmpc_amd.config_spec's layouts)
+    layout, dynamic = {0: ("nmpc_tt", False), 1: (None, False), 2: (None, False), 3: ("race_track_2", False),
+                       4: ("race_track_2", False), 5: ("dynamic", True)}[cfg]
+    prob = orc.make_problem(layout, N=spec_cfg.N, T=spec_cfg.T, dynamic=dynamic, model=spec_cfg.model)
+    assert prob.np_ == spec_cfg.np and prob.n_obs == spec_cfg.n_obs, "CPU baseline problem differs from the bench's"
+    # the W warm-up steps, untimed (the GPU runs them as W per-step launches), for as many
+    # scenarios as a warm-up budget allows (all 4,096 of config 3 take ~1 s; config 5's
+    # N = 50 solves are ~5x dearer): the timed window runs on the fully warmed ones
     P1, W1 = P, None
+    sel = np.arange(P.shape[0])
     if W > 0:
         r0 = cpu_ipopt.closed_loop(prob, P, W, lbx, ubx, lbg, ubg, orc.REFERENCE_OPTS, vt=12.0, wt=0.01,
-                                   p_step=None if p_step is None else p_step[:W], threads=nthr)
-        P1, W1 = r0["p"], r0["w"]
-    cpu_baseline.start = (P1, W1)
+                                   p_step=None if p_step is None else p_step[:W], threads=nthr,
+                                   budget_s=budget_s)
+        sel = np.flatnonzero(r0["steps"] == W)
+        P1, W1 = r0["p"][sel], r0["w"][sel]
+    cpu_baseline.start = (P1, W1, sel)
     t0 = time.perf_counter()
     r = cpu_ipopt.closed_loop(prob, P1, K, lbx, ubx, lbg, ubg, orc.REFERENCE_OPTS, vt=12.0, wt=0.01,
                               p_step=None if p_step is None else p_step[W:W + K], budget_s=budget_s,
@@ -129,6 +137,7 @@ def cpu_baseline(spec_cfg, cfg, P, lbx, ubx, lbg, ubg, K, W=0, p_step=None, budg
     done = r["steps"]
     n = int(done.sum())
     rows = np.flatnonzero(done > 0)
+    # records keyed by the row of the timed sample (P1 / W1 order)
     recs = [(int(b), k, int(r["status"][b, k]), r["u0"][b, k].copy(), float(r["f"][b, k]))
             for b in rows for k in range(int(done[b]))]
     cpu_baseline.records = recs
@@ -139,21 +148,22 @@ def cpu_baseline(spec_cfg, cfg, P, lbx, ubx, lbg, ubg, K, W=0, p_step=None, budg
     # cold-start leg (cold u = 0 and warm-started): every scenario's NLP of
     # the timed window's first step from u = 0, the same threads
     t1 = time.perf_counter()
-    rc = cpu_ipopt.solve_batch(prob, np.zeros((P.shape[0], spec_cfg.nw)), P1, lbx, ubx, lbg, ubg,
+    rc = cpu_ipopt.solve_batch(prob, np.zeros((P1.shape[0], spec_cfg.nw)), P1, lbx, ubx, lbg, ubg,
                                orc.REFERENCE_OPTS, threads=nthr)
     cwall = time.perf_counter() - t1
 
     def pct(v):
         return {"p50_ms": float(np.percentile(v, 50) * 1e3), "p99_ms": float(np.percentile(v, 99) * 1e3),
                 "max_ms": float(v.max() * 1e3)} if len(v) else None
-    cold = {"value": P.shape[0] / cwall, "unit": "NLP solves/s", "solves": int(P.shape[0]), "wall_s": cwall,
+    cold = {"value": P1.shape[0] / cwall, "unit": "NLP solves/s", "solves": int(P1.shape[0]), "wall_s": cwall,
             "mean_ip_iterations": float(rc["iter"].mean()), "per_solve_wall": pct(rc["solve_s"]),
             "status_histogram": {int(k): int(v) for k, v in zip(*np.unique(rc["status"], return_counts=True))},
-            "sample": f"cold solves (u = 0) of all {P.shape[0]} bench scenarios, {nthr} threads"}
+            "sample": f"cold solves (u = 0) of the timed window's first step, {P1.shape[0]} scenarios, {nthr} threads"}
     return {"value": n / wall, "unit": "MPC steps/s", "cores": nthr, "kind": "port",
             "sample": f"{n} warm-started closed-loop MPC steps (solve + shift) of the GPU's timed window -- "
                       f"steps {W}..{W + K - 1} after the same {W} untimed warm-up steps, up to {K} per scenario, "
-                      f"{len(rows)} of the bench's config-{cfg} scenarios -- by oracle/cpu_ipopt.cpp (CPU "
+                      f"{len(rows)} of the bench's config-{cfg} scenarios ({len(sel)} warmed within the budget) -- "
+                      f"by oracle/cpu_ipopt.cpp (CPU "
                       f"restatement, not CasADi: C++/OpenMP IPOPT restatement with a Riccati step), "
                       f"{nthr} threads, budget {budget_s:.0f}s, wall {wall:.1f}s",
             "mean_ip_iterations": float(its.mean()) if n else None,
@@ -176,7 +186,7 @@ def parity_sample(solver, spec, start, K, records, bnd, dev, p_step=None, tol=1e
         return None
     idx = {r: j for j, r in enumerate(rows)}
     B = len(rows)
-    P1, W1 = start
+    P1, W1, _ = start
     f64 = dict(dtype=torch.float64, device=dev)
     hist = {"u": torch.empty(K, B, 6, **f64), "f": torch.empty(K, B, **f64),
             "status": torch.empty(K, B, dtype=torch.int32, device=dev)}

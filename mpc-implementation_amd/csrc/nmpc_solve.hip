@@ -2531,13 +2531,13 @@ __device__ __forceinline__ void resto_phase(const Params* __restrict__ prm, doub
           auto sub_errR = [&](double mu_) {
             const double et = o.resto_proximity_weight * sqrt(mu_);
             double dn = 0.0, cm = 0.0, pinf = 0.0;
-            for (int i = S.lanef(); i < nw; i += WAVE) {
+            S.ctrls([&](int i, bool) {  // (maxima ignore the repeated last entry)
               const double g =
                   S.fixed(i) ? 0.0 : S.grad_u(i) + et * S.dr2(i) * (S.U[i] - S.UR[i]) - S.zl[i] + S.zu[i];
               dn = fmax(dn, fabs(g));
               if (S.hasl(S.xl[i])) cm = fmax(cm, fabs((S.U[i] - S.xl[i]) * S.zl[i] - mu_));
               if (S.hasu(S.xu[i])) cm = fmax(cm, fabs((S.xu[i] - S.U[i]) * S.zu[i] - mu_));
-            }
+            });
             S.rows([&](int r, bool on) {
               const double yr = S.y[r], vlr = S.vl[r], vur = S.vu[r], zp = S.zpR[r], zn = S.znR[r];
               const double sr = S.s[r], dr = S.d[r], pr = S.pR[r], nr = S.nR[r], lo = S.dl[r], hi = S.du[r];
