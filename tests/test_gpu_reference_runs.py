@@ -236,3 +236,54 @@ def test_reference_run_chained_and_fov_sum(name):
     assert n >= CHAIN_FACTOR * min(parts.values())
     assert abs(fg - fo) <= TOL * (1 + abs(fo))
     assert abs(fov_all - fov_ref) <= FOV_SPREAD_FACTOR * spread + TOL * (1 + abs(fov_ref))
+
+
+@pytest.mark.parametrize("name", RUN_NAMES)
+def test_reference_run_kkt_certificate(name):
+    """Independent of any solver's path: every step the GPU reports Solve_Succeeded is a
+    first-order point of the reference's NLP, re-evaluated with the oracle's function layer
+    (oracle.SSEval: the reference's dynamics, cost and rows, derivatives pinned to SymPy),
+    within IPOPT's unscaled acceptance thresholds, read on g(x) rather than on IPOPT's
+    slacks: dual infeasibility |grad f + J^T lam_g + lam_x|_inf <= dual_inf_tol = 1 and
+    <= 1e-4 (1 + |grad f|_inf), constraint violation <= constr_viol_tol = 1e-4,
+    complementarity |lam| * gap <= compl_inf_tol (1 + |lam|_inf) = 1e-4 (1 + |lam|_inf) (the
+    slacks differ from g(x) by up to the violation, which a multiplier of size |lam|
+    carries into the product: the oracle's own solutions of NMPC_TT.py reach 3e-4 at
+    |lam| ~ 1e2); lam_g, lam_x in CasADi's sign convention (> 0 on an upper bound)."""
+    from oracle import nmpc_oracle as orc
+    from nmpc_amd import nlpsol, REFERENCE_OPTS
+    from gen_reference_runs import run_spec, run_problem
+
+    z = _load(name)
+    prob = run_problem(name)
+    s = nlpsol("solver", "ipopt", run_spec(name), REFERENCE_OPTS)
+    W = _warm_starts(name, z)
+    sol = s(x0=W.T, lbx=z["lbx"], ubx=z["ubx"], lbg=z["lbg"], ubg=z["ubg"], p=z["p"].T)
+    st = s.stats()["status_code"]
+    lbx, ubx, lbg, ubg = z["lbx"], z["ubx"], z["lbg"], z["ubg"]
+    worst = {"stat": 0.0, "stat_rel": 0.0, "viol": 0.0, "compl": 0.0}
+    steps = np.flatnonzero(st == 0)
+    for k in steps:
+        x, lg, lx = sol["x"][:, k], sol["lam_g"][:, k], sol["lam_x"][:, k]
+        ev = orc.SSEval(prob, x, z["p"][k])
+        stat = float(np.max(np.abs(ev.gradF + ev.J.T @ lg + lx)))
+        gmax = float(np.max(np.abs(ev.gradF)))
+        viol = max(float(np.max(ev.g - ubg)), float(np.max(lbg - ev.g)), float(np.max(x - ubx)),
+                   float(np.max(lbx - x)), 0.0)
+
+        def cpl(lam, v, lo, hi):
+            up = np.where(lam > 0, lam * np.where(np.isfinite(hi), hi - v, 0.0), 0.0)
+            dn = np.where(lam < 0, -lam * np.where(np.isfinite(lo), v - lo, 0.0), 0.0)
+            return float(max(np.max(np.abs(up), initial=0.0), np.max(np.abs(dn), initial=0.0)))
+        lmax = max(float(np.max(np.abs(lg), initial=0.0)), float(np.max(np.abs(lx), initial=0.0)))
+        compl = max(cpl(lg, ev.g, lbg, ubg), cpl(lx, x, lbx, ubx)) / (1 + lmax)
+        worst["stat"] = max(worst["stat"], stat)
+        worst["stat_rel"] = max(worst["stat_rel"], stat / (1 + gmax))
+        worst["viol"] = max(worst["viol"], viol)
+        worst["compl"] = max(worst["compl"], compl)
+    print(f"\n{name}: {len(steps)} converged GPU steps certified; worst dual infeasibility {worst['stat']:.2e} "
+          f"({worst['stat_rel']:.2e} relative), constraint violation {worst['viol']:.2e}, "
+          f"complementarity {worst['compl']:.2e} (relative to 1 + |lam|)")
+    assert len(steps) > 0
+    assert worst["stat"] <= 1.0 and worst["stat_rel"] <= 1e-4
+    assert worst["viol"] <= 1e-4 and worst["compl"] <= 1e-4
