@@ -24,6 +24,7 @@ out = {"x": torch.empty(1, spec.nw, **f64), "f": torch.empty(1, **f64),
        "status": torch.empty(1, dtype=torch.int32, device="cuda"), "iters": torch.empty(1, dtype=torch.int32, device="cuda")}
 s.set_trace(True)
 tot_it = tot_ms = 0.0
+hist = {}  # (restoration?, trials) -> iterations over the timed steps
 for k in range(W + K):
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
@@ -38,7 +39,17 @@ for k in range(W + K):
     if k >= W:
         tot_it += n
         tot_ms += ms
+        for v in ls:
+            key = (bool(v < 0), int(abs(v)))
+            hist[key] = hist.get(key, 0) + 1
     print(f"step {k - W:3d}: it {n:3d} status {int(out['status'].item()):3d} resto {resto:3d} "
           f"ls trials mean {np.abs(ls).mean():5.2f} max {np.abs(ls).max():4.0f}  {ms:6.2f} ms  {1e3 * ms / max(n, 1):6.1f} us/it")
     s.shift_device(p, out["x"], w, vt, wt)
 print(f"timed steps: {tot_it:.0f} iterations in {tot_ms:.1f} ms alone on the GPU ({1e3 * tot_ms / tot_it:.1f} us/iteration)")
+for r in (False, True):
+    row = {t: c for (rr, t), c in sorted(hist.items()) if rr == r}
+    tot = sum(row.values())
+    if tot:
+        print(("restoration" if r else "regular") + f" iterations {tot}: line-search trials -> count " +
+              ", ".join(f"{t}:{c}" for t, c in row.items()) +
+              f"  (mean {sum(t * c for t, c in row.items()) / tot:.2f})")
