@@ -40,6 +40,12 @@
 // Named (not anonymous): the library is built as several translation units (one per
 // capacity class, compiled in parallel, plus the host side, NMPC_TU_CLASS / NMPC_TU_HOST)
 // that exchange kernel pointers whose signatures use these types.
+#ifndef NMPC_X_DZ
+#define NMPC_X_DZ 0
+#endif
+#ifndef NMPC_X_ASMD
+#define NMPC_X_ASMD 0
+#endif
 namespace nmpc_impl {
 
 constexpr int WAVE = 64;
@@ -152,7 +158,8 @@ constexpr Lay make_layout(int N, int m, bool lr, bool refine, bool eq) {
   const bool pin = 8 * NS >= 144;
   if (!pin) { L.P0 = o; o += 64; L.P1 = o; o += 64; L.pv0 = o; o += 8; L.pv1 = o; o += 8; }
   L.St = o; o += 48;
-  L.p = o; o += 64; L.ob = o; o += al2(2 * NMPC_MAX_OBS); L.inc = o; o += al2(8 * NS);
+  // inc: stage rows 0..N plus the -0.0 row N + 1 of the unrolled stage sums (Solver::kZeroRow)
+  L.p = o; o += 64; L.ob = o; o += al2(2 * NMPC_MAX_OBS); L.inc = o; o += al2(8 * (NS + 1));
   if (pin) { L.P0 = L.inc; L.P1 = L.inc + 64; L.pv0 = L.inc + 128; L.pv1 = L.inc + 136; }
 #ifdef NMPC_STAMPS
   L.red = o; o += 24;  // phase timers
@@ -355,6 +362,9 @@ struct Solver {
   // (fully unrolled, so their loads issue together) for classes up to 32 stages
   static constexpr bool kUnrollStages = CAP::nmax <= 32;
   static constexpr int kStageUnroll = kUnrollStages ? CAP::nmax : 1;
+  // row of `inc` past every stage row (make_layout): -0.0 entries, the additive identity
+  // that the unrolled prefix / suffix sums read where a lane's guard is off
+  static constexpr int kZeroRow = CAP::nmax + 1;
   const CST Params* __restrict__ P;
   LDS double* sm;
   int lane_, b;
@@ -498,15 +508,24 @@ struct Solver {
 #pragma unroll
       for (int c = 0; c < 5; ++c) inc[k * 8 + c] = T * uk(k * 6 + 1 + c);
     }
+    if (kUnrollStages && k < 8) inc[kZeroRow * 8 + k] = -0.0;
     sync();
     double a[5];
     if (k <= N) {
 #pragma unroll
       for (int c = 0; c < 5; ++c) a[c] = pp[3 + c];
-      const int jlim = kUnrollStages ? CAP::nmax : k;
-#pragma unroll kStageUnroll
-      for (int j = 0; j < jlim; ++j) {
-        if (j < k) {
+      if constexpr (kUnrollStages) {
+        // every lane reads a row per j -- its increment row while j < k, the -0.0 row
+        // otherwise (x + -0.0 == x exactly) -- so the reads carry no lane-dependent branch
+        // and issue together; the sums are bitwise the guarded in-order recursion
+#pragma unroll
+        for (int j = 0; j < CAP::nmax; ++j) {
+          const LDS double* ij = inc + (j < k ? j : kZeroRow) * 8;
+#pragma unroll
+          for (int c = 0; c < 5; ++c) a[c] = a[c] + ij[c];
+        }
+      } else {
+        for (int j = 0; j < k; ++j) {
 #pragma unroll
           for (int c = 0; c < 5; ++c) a[c] = a[c] + inc[j * 8 + c];
         }
@@ -521,10 +540,16 @@ struct Solver {
     sync();
     if (k <= N) {
       double c0 = pp[0], c1 = pp[1], c2 = pp[2];
-      const int jlim = kUnrollStages ? CAP::nmax : k;
-#pragma unroll kStageUnroll
-      for (int j = 0; j < jlim; ++j) {
-        if (j < k) {
+      if constexpr (kUnrollStages) {
+#pragma unroll
+        for (int j = 0; j < CAP::nmax; ++j) {
+          const LDS double* ij = inc + (j < k ? j : kZeroRow) * 8;
+          c0 = c0 + ij[5];
+          c1 = c1 + ij[6];
+          c2 = c2 + ij[7];
+        }
+      } else {
+        for (int j = 0; j < k; ++j) {
           c0 = c0 + inc[j * 8 + 5];
           c1 = c1 + inc[j * 8 + 6];
           c2 = c2 + inc[j * 8 + 7];
@@ -577,13 +602,36 @@ struct Solver {
     if (k <= N) {
       const LDS double* xk = Xs + k * 8;
       if (k < N) f = stage_cost(xk);
-      // unrolled over the layout's row capacity: the obstacle rows' square roots overlap
+      if constexpr (!CAP::deep) {  // register-limited classes: one row at a time (fewer live values)
 #pragma unroll
-      for (int i = 0; i < CAP::mmax; ++i) {
-        if (i < m) {
-          const int r = k * m + i;
-          const double g = row_value(xk, i);
-          dst[r] = scale ? scale[r] * g : g;
+        for (int i = 0; i < CAP::mmax; ++i) {
+          if (i < m) {
+            const int r = k * m + i;
+            const double g = row_value(xk, i);
+            dst[r] = scale ? scale[r] * g : g;
+          }
+        }
+      } else {
+        // unrolled over the layout's row capacity; every row value is formed unconditionally
+        // (clamped obstacle index) before the guarded stores, so the obstacle rows' loads and
+        // square roots overlap instead of running one row at a time behind the wave-uniform
+        // row-kind branches (same operations as row_value, so the same bits)
+        const double x0 = xk[0], x1 = xk[1];
+        double gv[CAP::mmax];
+#pragma unroll
+        for (int i = 0; i < CAP::mmax; ++i) {
+          const int oi = i - nb;
+          const int o = oi < 0 ? 0 : (oi < NMPC_MAX_OBS ? oi : NMPC_MAX_OBS - 1);
+          const double ddx = x0 - obx[o], ddy = x1 - oby[o];
+          const double ov = -sqrt(ddx * ddx + ddy * ddy) + P->orr[o];
+          gv[i] = i < 5 ? (i < nb ? xk[boxidx(i < 5 ? i : 0)] : ov) : ov;
+        }
+#pragma unroll
+        for (int i = 0; i < CAP::mmax; ++i) {
+          if (i < m) {
+            const int r = k * m + i;
+            dst[r] = scale ? scale[r] * gv[i] : gv[i];
+          }
         }
       }
     }
@@ -747,17 +795,25 @@ struct Solver {
 #pragma unroll
       for (int i = 0; i < 8; ++i) wv[k * 8 + i] = w[i];
     }
+    if (kUnrollStages && k < 8) wv[kZeroRow * 8 + k] = -0.0;
     sync();
     if (k <= N) {
       const int cs[6] = {0, 1, 2, 5, 6, 7};
       double acc[6];
 #pragma unroll
       for (int q = 0; q < 6; ++q) acc[q] = wv[N * 8 + cs[q]];
-      // suffix sums in the oracle's order (j = N-1 down to k), unrolled to the
-      // class maximum so the LDS reads pipeline
-#pragma unroll kStageUnroll
-      for (int jj = (kUnrollStages ? CAP::nmax : N) - 1; jj >= 0; --jj) {
-        if (jj < N && jj >= k) {
+      // suffix sums in the oracle's order (j = N-1 down to k), unrolled to the class
+      // maximum; a lane whose guard is off reads the -0.0 row (-0.0 + x == x exactly), so
+      // the reads carry no lane-dependent branch and pipeline
+      if constexpr (kUnrollStages) {
+#pragma unroll
+        for (int jj = CAP::nmax - 1; jj >= 0; --jj) {
+          const LDS double* wj = wv + ((jj < N && jj >= k) ? jj : kZeroRow) * 8;
+#pragma unroll
+          for (int q = 0; q < 6; ++q) acc[q] = wj[cs[q]] + acc[q];
+        }
+      } else {
+        for (int jj = N - 1; jj >= k; --jj) {
 #pragma unroll
           for (int q = 0; q < 6; ++q) acc[q] = wv[jj * 8 + cs[q]] + acc[q];
         }
@@ -768,9 +824,23 @@ struct Solver {
     sync();
     if (k <= N) {
       double a3 = wv[N * 8 + 3], a4 = wv[N * 8 + 4];
-#pragma unroll kStageUnroll
-      for (int j = (kUnrollStages ? CAP::nmax : N) - 1; j >= 0; --j) {
-        if (j < N && j >= k) {
+      if constexpr (kUnrollStages) {
+        // every lane evaluates each stage term (clamped stage index: valid reads, no
+        // lane-dependent branch) and keeps it only where its guard holds
+#pragma unroll
+        for (int j = CAP::nmax - 1; j >= 0; --j) {
+          const bool on = j < N && j >= k;
+          const int jc = j < N ? j : 0;
+          double E03, E04, E13, E14, E23, b00, b10, b20;
+          stage_AB(jc, E03, E04, E13, E14, E23, b00, b10, b20);
+          const LDS double* ln = lam + (jc + 1) * 8;
+          const double n3 = wv[jc * 8 + 3] + (((E03 * ln[0] + E13 * ln[1]) + E23 * ln[2]) + a3);
+          const double n4 = wv[jc * 8 + 4] + ((E04 * ln[0] + E14 * ln[1]) + a4);
+          a3 = on ? n3 : a3;
+          a4 = on ? n4 : a4;
+        }
+      } else {
+        for (int j = N - 1; j >= k; --j) {
           double E03, E04, E13, E14, E23, b00, b10, b20;
           stage_AB(j, E03, E04, E13, E14, E23, b00, b10, b20);
           const LDS double* ln = lam + (j + 1) * 8;
@@ -1262,6 +1332,47 @@ struct Solver {
       const LDS double* xk = X + k * 8;
       double Qxy0 = 0, Qxy1 = 0, Qxy2 = 0, qx = 0, qy = 0;
       double Qb[5] = {0, 0, 0, 0, 0}, qb[5] = {0, 0, 0, 0, 0};
+#if NMPC_X_ASMD
+      if constexpr (!CAP::lds_rows && kUnrollStages == false) {
+        // global-row classes: the stage's row operands (workspace, L2 / Infinity-Cache
+        // latency) fetched in blocks of five rows with clamped indices before the rows are
+        // folded in (the same per-row arithmetic and order as the loop below)
+        constexpr int BLK = 5;
+#pragma unroll
+        for (int i0 = 0; i0 < CAP::mmax; i0 += BLK) {
+          double wq[BLK], bq[BLK], yq[BLK], dq[BLK];
+#pragma unroll
+          for (int t = 0; t < BLK; ++t) {
+            const int i = i0 + t, ic = i < m ? i : m - 1, r = k * m + ic;
+            wq[t] = soc ? 0.0 : Wr[r]; bq[t] = Br[r];
+            yq[t] = y[r]; dq[t] = dc[r];
+          }
+#pragma unroll
+          for (int t = 0; t < BLK; ++t) {
+            const int i = i0 + t;
+            if (i < m) {
+              const double w = wq[t], bw = bq[t];
+              if (i < nb) {
+                Qb[i < 5 ? i : 0] = w;
+                qb[i < 5 ? i : 0] = bw;
+              } else {
+                const double C = curv ? yq[t] * dq[t] : 0.0;
+                const int o = i - nb;
+                const double ddx = xk[0] - obx[o], ddy = xk[1] - oby[o];
+                const double idd = rsq(ddx * ddx + ddy * ddy);
+                const double gx = -(ddx * idd), gy = -(ddy * idd);
+                const double id3 = idd * idd * idd;
+                Qxy0 += w * gx * gx + C * (-ddy * ddy * id3);
+                Qxy1 += w * gx * gy + C * (ddx * ddy * id3);
+                Qxy2 += w * gy * gy + C * (-ddx * ddx * id3);
+                qx += bw * gx;
+                qy += bw * gy;
+              }
+            }
+          }
+        }
+      } else
+#endif
       for (int i = 0; i < m; ++i) {
         const int r = k * m + i;
         const double w = soc ? 0.0 : Wr[r], bw = Br[r];
@@ -1441,7 +1552,16 @@ struct Solver {
         // R~ entry (rR, cR) of B^T P B, B = [b0 | T e_3..7] (lanes that carry no entry
         // compute entry 0 again: same value, so their store below needs no branch)
         R v;
-        if (rR == 0) {  // b0^T P[0:3,0:3] b0
+        if constexpr (CAP::deep) {  // the three entry kinds formed by every lane (their LDS reads valid for every lane,
+           // issued together) and selected by the lane's kind: no lane-dependent branch
+          const LDS R* Pr = Pc + (2 + rR) * 8;
+          const R pr0 = Pr[0], pr1 = Pr[1], pr2 = Pr[2], pe = Pc[(2 + rR) * 8 + 2 + cR];
+          const R va = b00 * ((P00 * b00 + P01 * b10) + P02 * b20) + b10 * ((P01 * b00 + P11 * b10) + P12 * b20) +
+                       b20 * ((P02 * b00 + P12 * b10) + P22 * b20);
+          const R vb = Tr * ((pr0 * b00 + pr1 * b10) + pr2 * b20);
+          const R vc = Tr * (Tr * pe);
+          v = rR == 0 ? va : (cR == 0 ? vb : vc);
+        } else if (rR == 0) {  // b0^T P[0:3,0:3] b0
           v = b00 * ((P00 * b00 + P01 * b10) + P02 * b20) + b10 * ((P01 * b00 + P11 * b10) + P12 * b20) +
               b20 * ((P02 * b00 + P12 * b10) + P22 * b20);
         } else if (cR == 0) {
@@ -2161,9 +2281,19 @@ struct Solver {
 
   // dual step components (oracle solve_dir) -- current slacks
   __device__ __forceinline__ void dz_x(int i, double dx, double& dzl, double& dzu) const {
-    dzl = 0.0; dzu = 0.0;
-    if (hasl(xl[i])) { const double iS = rcp(U[i] - xl[i]); dzl = mu * iS - zl[i] - zl[i] * iS * dx; }
-    if (hasu(xu[i])) { const double iS = rcp(xu[i] - U[i]); dzu = mu * iS - zu[i] + zu[i] * iS * dx; }
+    if constexpr (CAP::deep && NMPC_X_DZ) {
+      // loads hoisted and both sides formed, then selected (same arithmetic): the control
+      // passes' global loads are not issued one bound at a time behind lane-dependent branches
+      const double xli = xl[i], xui = xu[i], ui = U[i], zli = zl[i], zui = zu[i];
+      const bool hl = hasl(xli), hu = hasu(xui);
+      const double iSl = hl ? rcp(ui - xli) : 0.0, iSu = hu ? rcp(xui - ui) : 0.0;
+      dzl = hl ? mu * iSl - zli - zli * iSl * dx : 0.0;
+      dzu = hu ? mu * iSu - zui + zui * iSu * dx : 0.0;
+    } else {
+      dzl = 0.0; dzu = 0.0;
+      if (hasl(xl[i])) { const double iS = rcp(U[i] - xl[i]); dzl = mu * iS - zl[i] - zl[i] * iS * dx; }
+      if (hasu(xu[i])) { const double iS = rcp(xu[i] - U[i]); dzu = mu * iS - zu[i] + zu[i] * iS * dx; }
+    }
   }
   __device__ __forceinline__ void dv_s(int r, double dsv, double& dvl, double& dvu) const {
     dvl = 0.0; dvu = 0.0;
