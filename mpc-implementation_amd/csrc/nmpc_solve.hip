@@ -40,11 +40,8 @@
 // Named (not anonymous): the library is built as several translation units (one per
 // capacity class, compiled in parallel, plus the host side, NMPC_TU_CLASS / NMPC_TU_HOST)
 // that exchange kernel pointers whose signatures use these types.
-#ifndef NMPC_X_DZ
-#define NMPC_X_DZ 0
-#endif
-#ifndef NMPC_X_ASMD
-#define NMPC_X_ASMD 0
+#ifndef NMPC_X_ASM2
+#define NMPC_X_ASM2 0
 #endif
 namespace nmpc_impl {
 
@@ -782,13 +779,28 @@ struct Solver {
           const int r = k * m + nb + o;
           cyv[o] = o < nobs ? dc[r] * yy[r] : 0.0;
         }
+        if constexpr (CAP::deep) {
+          // every obstacle term formed (LDS reads valid for o < NMPC_MAX_OBS) and kept by a
+          // select: the rows' reads and square roots overlap
+          const double x0 = xk[0], x1 = xk[1];
 #pragma unroll
-        for (int o = 0; o < CAP::mmax - 5; ++o) {
-          if (o < nobs) {
-            const double ddx = xk[0] - obx[o], ddy = xk[1] - oby[o];
+          for (int o = 0; o < CAP::mmax - 5; ++o) {
+            const double ddx = x0 - obx[o], ddy = x1 - oby[o];
             const double idd = rsq(ddx * ddx + ddy * ddy);
-            w[0] += cyv[o] * (-(ddx * idd));
-            w[1] += cyv[o] * (-(ddy * idd));
+            const double n0 = w[0] + cyv[o] * (-(ddx * idd));
+            const double n1 = w[1] + cyv[o] * (-(ddy * idd));
+            w[0] = o < nobs ? n0 : w[0];
+            w[1] = o < nobs ? n1 : w[1];
+          }
+        } else {
+#pragma unroll
+          for (int o = 0; o < CAP::mmax - 5; ++o) {
+            if (o < nobs) {
+              const double ddx = xk[0] - obx[o], ddy = xk[1] - oby[o];
+              const double idd = rsq(ddx * ddx + ddy * ddy);
+              w[0] += cyv[o] * (-(ddx * idd));
+              w[1] += cyv[o] * (-(ddy * idd));
+            }
           }
         }
       }
@@ -859,7 +871,13 @@ struct Solver {
   __device__ __forceinline__ double grad_u(int i) const {
     const int k = i / 6, c = i - 6 * (i / 6);
     const LDS double* ln = lam + (k + 1) * 8;
-    if (c == 0) {
+    if constexpr (CAP::deep) {  // both forms from valid reads, then selected
+      const LDS double* tg = trig + k * 8;
+      const double ct = tg[0], stt = tg[1], cp = tg[2], sp = tg[3];
+      const double g0 = (T * cp * ct) * ln[0] + (T * sp * ct) * ln[1] + (T * stt) * ln[2];
+      const double gc = T * ln[2 + c];
+      return c == 0 ? g0 : gc;
+    } else if (c == 0) {
       const LDS double* tg = trig + k * 8;
       const double ct = tg[0], stt = tg[1], cp = tg[2], sp = tg[3];
       return (T * cp * ct) * ln[0] + (T * sp * ct) * ln[1] + (T * stt) * ln[2];
@@ -1332,20 +1350,22 @@ struct Solver {
       const LDS double* xk = X + k * 8;
       double Qxy0 = 0, Qxy1 = 0, Qxy2 = 0, qx = 0, qy = 0;
       double Qb[5] = {0, 0, 0, 0, 0}, qb[5] = {0, 0, 0, 0, 0};
-#if NMPC_X_ASMD
-      if constexpr (!CAP::lds_rows && kUnrollStages == false) {
-        // global-row classes: the stage's row operands (workspace, L2 / Infinity-Cache
-        // latency) fetched in blocks of five rows with clamped indices before the rows are
-        // folded in (the same per-row arithmetic and order as the loop below)
+#if NMPC_X_ASM2
+      if constexpr (CAP::deep) {
+        // rows in blocks of five: the block's LDS operands read up front (clamped rows, the
+        // empty asm keeps the reads ahead of the row branches), then each row folded in with
+        // the loop's own branches and arithmetic below
         constexpr int BLK = 5;
 #pragma unroll
         for (int i0 = 0; i0 < CAP::mmax; i0 += BLK) {
-          double wq[BLK], bq[BLK], yq[BLK], dq[BLK];
+          double wq[BLK], bq[BLK], yq[BLK], dq[BLK], oxq[BLK], oyq[BLK];
 #pragma unroll
           for (int t = 0; t < BLK; ++t) {
             const int i = i0 + t, ic = i < m ? i : m - 1, r = k * m + ic;
-            wq[t] = soc ? 0.0 : Wr[r]; bq[t] = Br[r];
-            yq[t] = y[r]; dq[t] = dc[r];
+            const int oc = ic >= nb ? ic - nb : 0;
+            wq[t] = soc ? 0.0 : Wr[r]; bq[t] = Br[r]; yq[t] = y[r]; dq[t] = dc[r];
+            oxq[t] = obx[oc]; oyq[t] = oby[oc];
+            asm volatile("" : "+v"(wq[t]), "+v"(bq[t]), "+v"(yq[t]), "+v"(dq[t]), "+v"(oxq[t]), "+v"(oyq[t]));
           }
 #pragma unroll
           for (int t = 0; t < BLK; ++t) {
@@ -1357,8 +1377,7 @@ struct Solver {
                 qb[i < 5 ? i : 0] = bw;
               } else {
                 const double C = curv ? yq[t] * dq[t] : 0.0;
-                const int o = i - nb;
-                const double ddx = xk[0] - obx[o], ddy = xk[1] - oby[o];
+                const double ddx = xk[0] - oxq[t], ddy = xk[1] - oyq[t];
                 const double idd = rsq(ddx * ddx + ddy * ddy);
                 const double gx = -(ddx * idd), gy = -(ddy * idd);
                 const double id3 = idd * idd * idd;
@@ -2281,7 +2300,7 @@ struct Solver {
 
   // dual step components (oracle solve_dir) -- current slacks
   __device__ __forceinline__ void dz_x(int i, double dx, double& dzl, double& dzu) const {
-    if constexpr (CAP::deep && NMPC_X_DZ) {
+    if constexpr (CAP::deep) {
       // loads hoisted and both sides formed, then selected (same arithmetic): the control
       // passes' global loads are not issued one bound at a time behind lane-dependent branches
       const double xli = xl[i], xui = xu[i], ui = U[i], zli = zl[i], zui = zu[i];
