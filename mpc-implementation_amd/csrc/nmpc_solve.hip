@@ -40,9 +40,6 @@
 // Named (not anonymous): the library is built as several translation units (one per
 // capacity class, compiled in parallel, plus the host side, NMPC_TU_CLASS / NMPC_TU_HOST)
 // that exchange kernel pointers whose signatures use these types.
-#ifndef NMPC_X_ASM2
-#define NMPC_X_ASM2 0
-#endif
 namespace nmpc_impl {
 
 constexpr int WAVE = 64;
@@ -1350,48 +1347,6 @@ struct Solver {
       const LDS double* xk = X + k * 8;
       double Qxy0 = 0, Qxy1 = 0, Qxy2 = 0, qx = 0, qy = 0;
       double Qb[5] = {0, 0, 0, 0, 0}, qb[5] = {0, 0, 0, 0, 0};
-#if NMPC_X_ASM2
-      if constexpr (CAP::deep) {
-        // rows in blocks of five: the block's LDS operands read up front (clamped rows, the
-        // empty asm keeps the reads ahead of the row branches), then each row folded in with
-        // the loop's own branches and arithmetic below
-        constexpr int BLK = 5;
-#pragma unroll
-        for (int i0 = 0; i0 < CAP::mmax; i0 += BLK) {
-          double wq[BLK], bq[BLK], yq[BLK], dq[BLK], oxq[BLK], oyq[BLK];
-#pragma unroll
-          for (int t = 0; t < BLK; ++t) {
-            const int i = i0 + t, ic = i < m ? i : m - 1, r = k * m + ic;
-            const int oc = ic >= nb ? ic - nb : 0;
-            wq[t] = soc ? 0.0 : Wr[r]; bq[t] = Br[r]; yq[t] = y[r]; dq[t] = dc[r];
-            oxq[t] = obx[oc]; oyq[t] = oby[oc];
-            asm volatile("" : "+v"(wq[t]), "+v"(bq[t]), "+v"(yq[t]), "+v"(dq[t]), "+v"(oxq[t]), "+v"(oyq[t]));
-          }
-#pragma unroll
-          for (int t = 0; t < BLK; ++t) {
-            const int i = i0 + t;
-            if (i < m) {
-              const double w = wq[t], bw = bq[t];
-              if (i < nb) {
-                Qb[i < 5 ? i : 0] = w;
-                qb[i < 5 ? i : 0] = bw;
-              } else {
-                const double C = curv ? yq[t] * dq[t] : 0.0;
-                const double ddx = xk[0] - oxq[t], ddy = xk[1] - oyq[t];
-                const double idd = rsq(ddx * ddx + ddy * ddy);
-                const double gx = -(ddx * idd), gy = -(ddy * idd);
-                const double id3 = idd * idd * idd;
-                Qxy0 += w * gx * gx + C * (-ddy * ddy * id3);
-                Qxy1 += w * gx * gy + C * (ddx * ddy * id3);
-                Qxy2 += w * gy * gy + C * (-ddx * ddx * id3);
-                qx += bw * gx;
-                qy += bw * gy;
-              }
-            }
-          }
-        }
-      } else
-#endif
       for (int i = 0; i < m; ++i) {
         const int r = k * m + i;
         const double w = soc ? 0.0 : Wr[r], bw = Br[r];
