@@ -227,6 +227,56 @@ def parity_sample(solver, spec, start, K, records, bnd, dev, p_step=None, tol=1e
             "reference": "oracle/cpu_ipopt.cpp (the cpu_baseline leg's own solves; pinned to oracle/nmpc_oracle.py by tests/test_cpu_restatement.py)"}
 
 
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def rank_launch_cmd(n, argv, port):
+    """The command bench.py --gpus N runs when no launcher started it: one process per GPU
+    through torch.distributed.run on this node (127.0.0.1 rendezvous), each rank running
+    this same script with the same arguments (WORLD_SIZE is then set, so no rank relaunches)."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
+            "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__), *argv]
+
+
+def launch_ranks(n, argv):
+    """Parent of an N-rank run: starts the ranks as a child process (never exec: this
+    process stays the parent and has touched no GPU), streams every non-JSON line to
+    stderr as it arrives, and prints rank 0's JSON line last on stdout.  Returns the
+    launcher's exit code (non-zero also when no JSON line came back)."""
+    import subprocess
+    import threading
+
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC for RCCL (the host driver's only mode)
+    proc = subprocess.Popen(rank_launch_cmd(n, argv, _free_port()), stdout=subprocess.PIPE, env=env, text=True,
+                            bufsize=1)
+    lines = []
+
+    def pump():
+        for ln in proc.stdout:
+            if ln.lstrip().startswith("{"):
+                lines.append(ln.strip())
+            else:
+                sys.stderr.write(ln)
+                sys.stderr.flush()
+    t = threading.Thread(target=pump, daemon=True)
+    t.start()
+    rc = proc.wait()
+    t.join()
+    if lines:
+        print(lines[-1], flush=True)
+    elif rc == 0:
+        sys.stderr.write("bench.py: the ranks exited without a JSON line\n")
+        rc = 1
+    return rc
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -246,6 +296,16 @@ def main():
                     help="fused mode: rank 0 saves the gathered (scenarios, 8K) per-step rows (u0, f, status) "
                          "of the timed launch to this .npy (multi-rank rehearsal test)")
     args = ap.parse_args()
+    if args.gpus < 1:
+        raise SystemExit(f"bench.py: --gpus must be >= 1 (got {args.gpus})")
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        # no launcher around us: start the N rank processes ourselves (before any GPU call
+        # of this process, which never initialises the GPU) and relay rank 0's line
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+    if env_world is not None and int(env_world) != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} does not match the launcher's WORLD_SIZE={env_world}; "
+                         f"the line would be mislabelled")
 
     import torch
     import torch.distributed as dist

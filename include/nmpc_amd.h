@@ -138,11 +138,11 @@ int nmpc_dims(const nmpc_handle* h, int32_t* nw, int32_t* ng, int32_t* np, int32
  * Bounds as IPOPT reads them: |b| >= 1e19 is no bound; lbx == ubx fixes a variable
  * (fixed_variable_treatment = make_parameter: held at the bound, no step, lam_x 0);
  * rows with lbg == ubg are IPOPT's equality constraints c(x) = g(x) - lbg = 0 (no slack,
- * no relaxation; augmented-system step with IPOPT's inertia test), up to 64
+ * no relaxation; augmented-system step with IPOPT's inertia test), up to 128
  * per scenario.  A batch with any equality row runs on the equality class (global rows,
  * any shape): the host enqueues a bounds scan and both classes, and a device flag lets
  * exactly one of them run (no host round trip; the same for the _dev entry points).
- * lbx > ubx, more than 64 equality rows, or equality rows with the fp32 Riccati leg
+ * lbx > ubx, more than 128 equality rows, or equality rows with the fp32 Riccati leg
  * report status -11 (IPOPT Invalid_Problem_Definition) for that scenario. */
 int nmpc_solve_batch(nmpc_handle* h, int32_t B,
                      const double* x0, int64_t ld_x0,
@@ -167,13 +167,15 @@ int nmpc_solve_batch_dev(nmpc_handle* h, int32_t B,
 /* Optional per-iteration trace (debugging / parity): when enabled, the next
  * solve records NMPC_TRACE_FIELDS doubles per iteration per scenario into a
  * device buffer readable with nmpc_read_trace (host pointer,
- * B x (max_iter+3) x NMPC_TRACE_FIELDS, row-major; the last three rows of each
- * scenario are reserved for diagnostic phase timers).  Row i holds
+ * B x (max_iter+3) x NMPC_TRACE_FIELDS, row-major; the last two rows of each
+ * scenario are reserved for diagnostic phase timers).  Row i (0 <= i <= max_iter) holds
  *   [0..7]  {iter, mu, f_scaled, theta, delta_w, alpha_pr, alpha_du, ls_trials}
- *           after iteration i+1 (ls_trials < 0: a restoration iteration), and
- *   [8..11] the main phase's convergence check at iteration count i:
+ *           after iteration i+1 (ls_trials < 0: a restoration iteration; i < max_iter), and
+ *   [8..11] the convergence check at iteration count i:
  *           {scaled NLP error, dual infeasibility / s_d, constraint violation,
- *            complementarity / s_c} (IpoptCalculatedQuantities::curr_nlp_error). */
+ *            complementarity / s_c} (IpoptCalculatedQuantities::curr_nlp_error); a
+ *           NEGATIVE (sign bit set) error marks the restoration NLP's own check
+ *           (RestoIpoptNLP), which replaces the main check recorded at the same count. */
 #define NMPC_TRACE_FIELDS 12
 int nmpc_set_trace(nmpc_handle* h, int32_t enable);
 int nmpc_read_trace(nmpc_handle* h, int32_t B, double* host_out);
@@ -261,6 +263,13 @@ const char* nmpc_build_id(void);
 
 /* Launch geometry / workspace of the last solve, for measurement. */
 int nmpc_kernel_info(const nmpc_handle* h, int32_t* lds_bytes, int32_t* threads_per_scenario);
+
+/* Device workspace the handle holds (bytes): the problem class's per-scenario
+ * workspace, and the equality class's, which is allocated only once a
+ * batch with equality rows (lbg == ubg) has been solved and is 0 until then; per
+ * scenario: the class layouts' sizes (ws_per_scenario, wsE_per_scenario; nullable). */
+int nmpc_memory_info(const nmpc_handle* h, int64_t* ws_bytes, int64_t* ws_eq_bytes, int64_t* ws_per_scenario,
+                     int64_t* wsE_per_scenario);
 
 #ifdef __cplusplus
 }

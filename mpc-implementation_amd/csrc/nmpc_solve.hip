@@ -161,7 +161,7 @@ constexpr Lay make_layout(int N, int m, bool lr, bool refine, bool eq) {
   L.red = o;
 #endif
   if (lr) { L.dl = o; o += al2(ng); L.du = o; o += al2(ng); }  // row bounds (constant during a solve, read by every row pass)
-  L.rvars = o; o += 48;  // line-search / restoration scalars; [32..36] barrier sums; [40..45] watchdog; [46] #fixed
+  L.rvars = o; o += 48;  // line-search / restoration scalars; [32..36] barrier sums; [37..39] line-search powers (restoration: [23] flag, [37..38]); [40..45] watchdog; [46] #fixed
   L.fixm = o; o += al2(N / 2 + 1);  // fixed-control masks, one int per stage
   L.rdX = o; if (refine) o += al2(nX);  // refinement step in X (fp32 classes)
   if (lr) {
@@ -346,6 +346,22 @@ enum Phase { PH_ROLLOUT, PH_EVAL, PH_DERIVS, PH_ADJ, PH_SUMM, PH_RIC, PH_RESOLVE
 #else
 #define STAMP0() do {} while (0)
 #define STAMP1(ph) do {} while (0)
+#endif
+// -DNMPC_RESTO_TRIAL_STAMPS (diagnostics, with NMPC_STAMPS): the slots PH_BARR / PH_FTB /
+// PH_DFTB record the restoration line search instead -- cycles inside trial_resto, cycles
+// of second-order-correction blocks, number of trial_resto calls
+#if defined(NMPC_STAMPS) && defined(NMPC_RESTO_TRIAL_STAMPS)
+#define STAMP1G(ph) do {} while (0)
+#define RSTAMP0(v) STAMPV0(v)
+#define RSTAMP1(v, ph) STAMPV1(v, ph)
+#define RCOUNT(ph) do { if (lanef() == 0) stamps[ph] += 1.0; } while (0)
+#else
+#define STAMP1G(ph) STAMP1(ph)
+#define RSTAMP0(v) do {} while (0)
+#define RSTAMP1(v, ph) do {} while (0)
+#define RCOUNT(ph) do {} while (0)
+#endif
+#ifndef NMPC_STAMPS
 #define STAMPV0(v) do {} while (0)
 #define STAMPV1(v, ph) do {} while (0)
 #endif
@@ -934,7 +950,7 @@ struct Solver {
     barrier_ctrl(u, logs, damp);
     rows([&](int r, bool on) { barrier_row(r, on, dsv ? sb[r] + a * dsv[r] : sb[r], logs, damp); });
     const double rr = barrier_fin(f, logs, damp);
-    STAMP1(PH_BARR);
+    STAMP1G(PH_BARR);
     return rr;
   }
 
@@ -2167,6 +2183,8 @@ struct Solver {
                                               double& phit, double& tht) {
     // the trial controls, their barrier terms and the proximity term in one pass (each
     // accumulator keeps the per-lane order of barrier_obj / resto_pn_terms)
+    RSTAMP0(_trs);
+    RCOUNT(PH_DFTB);
     double th = 0.0, logs = 0.0, damp = 0.0, pn = 0.0, lg = 0.0, prox = 0.0;
     ctrls([&](int i, bool on) {
       const double ui = U[i] + a * dUs[i];
@@ -2199,6 +2217,7 @@ struct Solver {
     pn = wsum(pn); lg = wsum(lg); prox = wsum(prox);
     rvars[34] = pn; rvars[35] = lg; rvars[36] = prox;
     phit = phb + pn_of(pn, lg, prox);
+    RSTAMP1(_trs, PH_BARR);
     return isfinite(phit);
   }
   __device__ __forceinline__ double frac_to_bound_resto(double tau_, const GLB double* dUs, const RV* dss,
@@ -2249,7 +2268,7 @@ struct Solver {
       extra(r, on);
     });
     a = wmin(a);
-    STAMP1(PH_FTB);
+    STAMP1G(PH_FTB);
     return a;
   }
 
@@ -2300,7 +2319,7 @@ struct Solver {
       extra(r, on);
     });
     a = wmin(a);
-    STAMP1(PH_DFTB);
+    STAMP1G(PH_DFTB);
     return a;
   }
 
@@ -2616,6 +2635,10 @@ __device__ __forceinline__ void resto_phase(const Params* __restrict__ prm, doub
         V[13] = fmax(smax, (sumy + sumz + sumv + sump) / ndR) / smax;
         V[14] = fmax(smax, (sumz + sumv + sump) / ncR) / smax;
         const double errR = fmax(fmax(dinf / V[13], cv), cmr / V[14]);
+        if (trace && S.lanef() == 0) {  // the restoration NLP's convergence check at `it` (parity
+          double* t = trace + (long long)it * TRACE_F;  // diagnostics; negative error: a restoration check)
+          t[8] = -errR; t[9] = dinf / V[13]; t[10] = cv; t[11] = cmr / V[14];
+        }
         if (wany(bad) || !isfinite(errR)) { rstat = ST_INVALID_NUMBER; break; }
         const bool conv = errR <= o.tol && dinf <= o.dual_inf_tol && cv <= o.constr_viol_tol && cmr <= o.compl_inf_tol;
         if (it != rlast_it) { V[10] = V[11]; V[11] = rho * frp + 0.5 * S.etaR * frx; rlast_it = it; }
@@ -2744,8 +2767,21 @@ __device__ __forceinline__ void resto_phase(const Params* __restrict__ prm, doub
           V[6] = o.theta_max_fact * fmax(1.0, V[15]);
           V[7] = o.theta_min_fact * fmax(1.0, V[15]);
         }
+        // the switching condition's powers of the reference values V[15], V[16], formed once
+        // when first needed (V[23]: valid flag, reset wherever V[15] / V[16] change; the main
+        // phase's twin, PW, uses the same slots -- the two phases never overlap)
+        V[23] = 0.0;
+        auto r_pw = [&]() {
+          if (V[23] == 0.0) {
+            V[37] = V[16] < 0.0 ? pow(-V[16], o.s_phi) : 0.0;
+            V[38] = pow(V[15], o.s_theta);
+            V[23] = 1.0;
+          }
+        };
         auto r_ftype = [&](double a) {
-          return V[16] < 0.0 && a * pow(-V[16], o.s_phi) > o.delta * pow(V[15], o.s_theta);
+          if (!(V[16] < 0.0)) return false;
+          r_pw();
+          return a * V[37] > o.delta * V[38];
         };
         auto r_armijo = [&](double a, double ph) { return cmp_le(ph - V[17], o.eta_phi * a * V[16], V[17]); };
         auto r_check = [&](double a_test, double ph, double th) {
@@ -2781,7 +2817,7 @@ __device__ __forceinline__ void resto_phase(const Params* __restrict__ prm, doub
           rin_wd = true;
           rwd_trial = 0;
         }
-        if (rin_wd) { V[15] = WD[0]; V[16] = WD[1]; V[17] = WD[2]; }
+        if (rin_wd) { V[15] = WD[0]; V[16] = WD[1]; V[17] = WD[2]; V[23] = 0.0; }
         auto rwd_restore = [&]() {  // StopWatchDog
           for (int i = S.lanef(); i < nw; i += WAVE) {
             S.U[i] = S.wU[i]; S.zl[i] = S.wzl[i]; S.zu[i] = S.wzu[i]; S.dU[i] = S.wdU[i];
@@ -2795,7 +2831,7 @@ __device__ __forceinline__ void resto_phase(const Params* __restrict__ prm, doub
           S.rollout(S.U, S.X);
           V[12] = S.df * S.eval_fg(S.X, S.d, S.dc);
           S.derivs(S.X, S.U);
-          V[15] = WD[0]; V[16] = WD[1]; V[17] = WD[2];
+          V[15] = WD[0]; V[16] = WD[1]; V[17] = WD[2]; V[23] = 0.0;
           S.delta = WD[5];
           rwd_dir = true;
           rftb_ok = false;
@@ -2824,7 +2860,10 @@ __device__ __forceinline__ void resto_phase(const Params* __restrict__ prm, doub
         double amin = o.gamma_theta;
         if (V[16] < 0) {
           amin = fmin(o.gamma_theta, o.gamma_phi * V[15] / (-V[16]));
-          if (V[15] <= V[7]) amin = fmin(amin, o.delta * pow(V[15], o.s_theta) / pow(-V[16], o.s_phi));
+          if (V[15] <= V[7]) {
+            r_pw();
+            amin = fmin(amin, o.delta * V[38] / V[37]);
+          }
         }
         amin *= o.alpha_min_frac;
         a = rskip ? V[18] * o.alpha_red_factor : V[18];
@@ -2834,6 +2873,7 @@ __device__ __forceinline__ void resto_phase(const Params* __restrict__ prm, doub
           const bool ok_t = S.trial_resto(a, S.dU, S.ds, S.dpR, S.dnR, fo_t, ph, th);
           if (ok_t && r_check(a, ph, th)) { acc = 1; V[19] = a; V[20] = fo_t; V[21] = ph; a_test = a; break; }
           if (ok_t && a == V[18] && V[15] <= th && o.max_soc > 0) {
+            RSTAMP0(_soc);
             double th_tr = th, th_old = 0.0, a_soc = a;
             for (int r = S.lanef(); r < ng; r += WAVE) S.cms[r] = S.d[r] - S.s[r] - S.pR[r] + S.nR[r];
             sync();
@@ -2872,6 +2912,7 @@ __device__ __forceinline__ void resto_phase(const Params* __restrict__ prm, doub
               ++cnt;
               th_tr = th2;
             }
+            RSTAMP1(_soc, PH_FTB);
             if (soc_ok) break;
           }
           a *= o.alpha_red_factor;
@@ -3489,6 +3530,19 @@ __device__ __forceinline__ int solve_one(Solver<CAP>& S, const Params* __restric
 
     // ===== line search (BacktrackingLineSearch + FilterLSAcceptor)
     double theta_ref = 0.0, gbd = 0.0, tiny_mx = 0.0, tiny_msv = 0.0;
+    // the switching condition's powers pow(-gbd, s_phi), pow(theta_ref, s_theta) depend only
+    // on the line search's reference values: formed once (when first needed) and reused by
+    // every trial's F-type test, the minimum step and the filter decision, the same doubles
+    // as one pow per use (PW[0]: valid flag; reset wherever theta_ref / gbd change)
+    volatile LDS double* PW = S.rvars + 37;
+    PW[0] = 0.0;
+    auto pw_get = [&]() {
+      if (PW[0] == 0.0) {
+        PW[1] = gbd < 0.0 ? pow(-gbd, o.s_phi) : 0.0;
+        PW[2] = pow(theta_ref, o.s_theta);
+        PW[0] = 1.0;
+      }
+    };
     // primal / dual fraction to the boundary of the step (dU, ds) at the current iterate,
     // formed with the step's row pass; valid until the watchdog restores another iterate
     double ftb_p = 1.0, ftb_d = 1.0;
@@ -3520,6 +3574,7 @@ __device__ __forceinline__ int solve_one(Solver<CAP>& S, const Params* __restric
       }
       theta_ref = wsum(th);
       gbd = wsum(g);
+      PW[0] = 0.0;  // new reference values: the switching-condition powers are formed anew
       tiny_mx = wmax(mx);
       tiny_msv = wmax(msv);
       STAMP1(PH_LSSET);
@@ -3533,7 +3588,9 @@ __device__ __forceinline__ int solve_one(Solver<CAP>& S, const Params* __restric
     const double eps = 2.220446049250313e-16;
     auto cmp_le = [&](double lhs, double rhs, double bas) { return lhs - rhs <= 10.0 * eps * fabs(bas); };
     auto is_ftype = [&](double a) {
-      return gbd < 0.0 && a * pow(-gbd, o.s_phi) > o.delta * pow(theta_ref, o.s_theta);
+      if (!(gbd < 0.0)) return false;
+      pw_get();
+      return a * PW[1] > o.delta * PW[2];
     };
     auto armijo = [&](double a, double phit) { return cmp_le(phit - phi_ref, o.eta_phi * a * gbd, phi_ref); };
     auto acc_iter = [&](double phit, double tht) {
@@ -3587,6 +3644,7 @@ __device__ __forceinline__ int solve_one(Solver<CAP>& S, const Params* __restric
       S.derivs(S.X, S.U);
       S.adjoint(S.df, S.y);  // grad of the Lagrangian there (soft restoration's pd error)
       theta_ref = WD[0]; phi_ref = WD[1]; gbd = WD[2];
+      PW[0] = 0.0;
       S.delta = WD[5];
       wd_dir = true;
       ftb_ok = false;  // another iterate and step: the fused fractions no longer apply
@@ -3618,6 +3676,7 @@ __device__ __forceinline__ int solve_one(Solver<CAP>& S, const Params* __restric
     }
     if (in_wd) {  // FilterLSAcceptor::InitThisLineSearch(in_watchdog): the stored reference
       theta_ref = WD[0]; phi_ref = WD[1]; gbd = WD[2];
+      PW[0] = 0.0;
     }
 
     // soft restoration step (BacktrackingLineSearch::TrySoftRestoStep); returns
@@ -3735,8 +3794,10 @@ __device__ __forceinline__ int solve_one(Solver<CAP>& S, const Params* __restric
         double amin = o.gamma_theta;
         if (gbd < 0) {
           amin = fmin(o.gamma_theta, o.gamma_phi * theta_ref / (-gbd));
-          if (theta_ref <= MV[1])
-            amin = fmin(amin, o.delta * pow(theta_ref, o.s_theta) / pow(-gbd, o.s_phi));
+          if (theta_ref <= MV[1]) {
+            pw_get();
+            amin = fmin(amin, o.delta * PW[2] / PW[1]);
+          }
         }
         amin *= o.alpha_min_frac;
         const double amax_p = ftb_ok ? ftb_p : S.frac_to_bound(tau, S.dU, S.ds);
@@ -4004,7 +4065,8 @@ __device__ __forceinline__ int solve_one(Solver<CAP>& S, const Params* __restric
     sync();
     if (S.lanef() == 0) stamps[PH_TOTAL] = (double)(__builtin_amdgcn_s_memtime() - _tk0);
     sync();
-    if (S.lanef() < PH_COUNT) trace[(long long)max_iter * TRACE_F + S.lanef()] = stamps[S.lanef()];
+    // rows max_iter + 1, max_iter + 2 (row max_iter holds the convergence check at iteration max_iter)
+    if (S.lanef() < PH_COUNT) trace[(long long)(max_iter + 1) * TRACE_F + S.lanef()] = stamps[S.lanef()];
   }
 #endif
   if (S.lanef() == 0) {
@@ -4484,6 +4546,12 @@ struct nmpc_handle {
   int lds_bytesE = 0;
   int residentE = 0;
   int* deq = nullptr;          // the gate flag (nmpc_eq_scan_kernel)
+  // the equality class's own workspace (its layout: global rows up to N = 63 and the
+  // 128 x 128 Schur storage, ~840 KB per scenario): allocated only once a batch with
+  // equality rows is seen, so handles whose batches have none carry only their class's
+  int ws_doublesE = 0;
+  double* dwsE = nullptr;
+  size_t wsE_bytes = 0;
   int resident = 0;            // closed-loop waves resident at once (occupancy x CUs)
   int* dsched = nullptr;       // step-queue scheduler state
   size_t sched_bytes = 0;
@@ -4541,15 +4609,67 @@ static int eq_gate(nmpc_handle* h, int B, const IO& io, hipStream_t st) {
   return NMPC_OK;
 }
 
-static int ensure_ws(nmpc_handle* h, int B) {
-  const size_t need = (size_t)B * h->ws_doubles * sizeof(double);
-  if (need > h->ws_bytes) {
-    if (h->dws) hipFree(h->dws);
-    h->dws = nullptr; h->ws_bytes = 0;
-    if (hipMalloc(&h->dws, need) != hipSuccess) return fail(NMPC_E_NOMEM, "hipMalloc workspace");
-    h->ws_bytes = need;
+static int ensure_buf(double** buf, size_t* bytes, size_t need, const char* what) {
+  if (need > *bytes) {
+    if (*buf) hipFree(*buf);
+    *buf = nullptr; *bytes = 0;
+    if (hipMalloc(buf, need) != hipSuccess) return fail(NMPC_E_NOMEM, std::string("hipMalloc ") + what);
+    *bytes = need;
   }
   return NMPC_OK;
+}
+static int ensure_ws(nmpc_handle* h, int B) {
+  return ensure_buf(&h->dws, &h->ws_bytes, (size_t)B * h->ws_doubles * sizeof(double), "workspace");
+}
+
+// Which kernels of the class pair a launch runs.  The equality class's workspace is
+// allocated lazily: while it does not cover B, the batch's bounds are scanned on the
+// device and the flag read back (one stream synchronisation), and only the class that
+// applies is launched -- the problem's own class when the batch has no equality row (its
+// workspace alone), the equality class (workspace allocated now) when it has.  Once that
+// workspace exists the pair is enqueued behind the device flag with no host round trip.
+// host_eq: -1 unknown (device pointers), 0 / 1 the host-side scan's answer.
+struct Run { bool A, E; };
+static int eq_prepare(nmpc_handle* h, int B, IO& io, IO& ioE, hipStream_t st, int host_eq, Run* run) {
+  ioE = io;
+  io.eqflag = nullptr; ioE.eqflag = nullptr;
+  run->A = true; run->E = false;
+  if (!h->kernE) return NMPC_OK;  // fp32 leg, or NMPC_FORCE_CLASS=E: one class, no partner
+  const size_t needE = (size_t)B * h->ws_doublesE * sizeof(double);
+  int eq = host_eq;
+  if (eq < 0 && needE > h->wsE_bytes) {
+    if (int rc = eq_gate(h, B, io, st)) return rc;
+    int flag = 0;
+    if (hipMemcpyAsync(&flag, h->deq, sizeof(int), hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipStreamSynchronize(st) != hipSuccess)
+      return fail(NMPC_E_HIP, "reading the equality-row flag");
+    eq = flag != 0;
+  }
+  if (eq >= 0) {  // known: launch the one class that applies
+    run->A = eq == 0; run->E = eq == 1;
+  } else {  // equality workspace in place: the gated pair, decided on the device
+    if (int rc = eq_gate(h, B, io, st)) return rc;
+    run->A = run->E = true;
+    io.eqflag = h->deq; ioE.eqflag = h->deq;
+  }
+  if (run->E) {
+    if (int rc = ensure_buf(&h->dwsE, &h->wsE_bytes, needE, "equality-class workspace")) return rc;
+    ioE.ws = h->dwsE;
+  }
+  return NMPC_OK;
+}
+
+// host-pointer bounds: does any scenario have a row with lbg == ubg (finite)?  (the test of
+// nmpc_eq_scan_kernel, on the caller's arrays before they are uploaded)
+static int host_has_eq(int B, int ng, const double* lbg, int64_t ld_lbg, const double* ubg, int64_t ld_ubg) {
+  for (int b = 0; b < B; ++b) {
+    const double* lo = lbg + (size_t)b * ld_lbg;
+    const double* hi = ubg + (size_t)b * ld_ubg;
+    for (int r = 0; r < ng; ++r)
+      if (lo[r] == hi[r] && lo[r] > -BIGB) return 1;
+    if (ld_lbg == 0 && ld_ubg == 0) break;
+  }
+  return 0;
 }
 
 extern "C" {
@@ -4643,7 +4763,7 @@ int nmpc_create(const nmpc_desc* desc, nmpc_handle** out) {
     if (!P.o.linear_solver_fp32 && !forcedE) {
       const ClassFns ce = nmpc_class_fns_E();
       h->kernE = ce.fn; h->loopE = ce.lfn; h->schedE = ce.sfn; h->lds_bytesE = ce.lds_doubles * 8;
-      if (ce.ws_doubles > h->ws_doubles) h->ws_doubles = ce.ws_doubles;
+      h->ws_doublesE = ce.ws_doubles;
     }
   }
   if (const char* e = std::getenv("NMPC_LDS_BYTES")) {  // diagnostics: pad LDS to cap workgroups per CU
@@ -4713,6 +4833,7 @@ int nmpc_destroy(nmpc_handle* h) {
   if (h->ibuf) hipFree(h->ibuf);
   if (h->dtrace) hipFree(h->dtrace);
   if (h->dws) hipFree(h->dws);
+  if (h->dwsE) hipFree(h->dwsE);
   if (h->dsched) hipFree(h->dsched);
   if (h->dtimes) hipFree(h->dtimes);
   if (h->deq) hipFree(h->deq);
@@ -4736,6 +4857,16 @@ int nmpc_kernel_info(const nmpc_handle* h, int32_t* lds_bytes, int32_t* tps) {
   return NMPC_OK;
 }
 
+int nmpc_memory_info(const nmpc_handle* h, int64_t* ws_bytes, int64_t* ws_eq_bytes, int64_t* ws_per_scenario,
+                     int64_t* wsE_per_scenario) {
+  if (!h) return fail(NMPC_E_INVALID, "null handle");
+  if (ws_bytes) *ws_bytes = (int64_t)h->ws_bytes;
+  if (ws_eq_bytes) *ws_eq_bytes = (int64_t)h->wsE_bytes;
+  if (ws_per_scenario) *ws_per_scenario = (int64_t)h->ws_doubles * 8;
+  if (wsE_per_scenario) *wsE_per_scenario = (int64_t)h->ws_doublesE * 8;
+  return NMPC_OK;
+}
+
 int nmpc_set_trace(nmpc_handle* h, int32_t enable) {
   if (!h) return fail(NMPC_E_INVALID, "null handle");
   h->trace = enable != 0;
@@ -4751,11 +4882,11 @@ int nmpc_read_trace(nmpc_handle* h, int32_t B, double* host_out) {
   return NMPC_OK;
 }
 
-int nmpc_solve_batch_dev(nmpc_handle* h, int32_t B, const double* x0, int64_t ld_x0, const double* lbx,
-                         int64_t ld_lbx, const double* ubx, int64_t ld_ubx, const double* lbg, int64_t ld_lbg,
-                         const double* ubg, int64_t ld_ubg, const double* p, int64_t ld_p, double* x_out,
-                         double* f_out, double* g_out, double* lam_x_out, double* lam_g_out, double* lam_p_out,
-                         double* X_out, int32_t* status, int32_t* iters, void* stream) {
+static int solve_dev(nmpc_handle* h, int32_t B, const double* x0, int64_t ld_x0, const double* lbx,
+                     int64_t ld_lbx, const double* ubx, int64_t ld_ubx, const double* lbg, int64_t ld_lbg,
+                     const double* ubg, int64_t ld_ubg, const double* p, int64_t ld_p, double* x_out,
+                     double* f_out, double* g_out, double* lam_x_out, double* lam_g_out, double* lam_p_out,
+                     double* X_out, int32_t* status, int32_t* iters, void* stream, int host_eq) {
   if (!h) return fail(NMPC_E_INVALID, "null handle");
   if (B < 0) return fail(NMPC_E_INVALID, "B < 0");
   if (B == 0) return NMPC_OK;
@@ -4771,7 +4902,6 @@ int nmpc_solve_batch_dev(nmpc_handle* h, int32_t B, const double* x0, int64_t ld
   io.x_out = x_out; io.f_out = f_out; io.g_out = g_out; io.lam_x = lam_x_out; io.lam_g = lam_g_out;
   io.lam_p = lam_p_out;
   io.X_out = X_out; io.status = status; io.iters = iters; io.trace = nullptr;
-  io.eqflag = h->kernE ? h->deq : nullptr;
   if (h->trace) {
     const size_t need = (size_t)B * (P.o.max_iter + 3) * TRACE_F * sizeof(double);
     if (need > h->trace_bytes) {
@@ -4786,17 +4916,27 @@ int nmpc_solve_batch_dev(nmpc_handle* h, int32_t B, const double* x0, int64_t ld
   if (int rc = ensure_ws(h, B)) return rc;
   io.ws = h->dws;
   h->last_B = B;
-  if (h->kernE) {
-    if (int rc = eq_gate(h, B, io, (hipStream_t)stream)) return rc;
-  }
-  hipLaunchKernelGGL(h->kern, dim3(B), dim3(WAVE), h->lds_bytes, (hipStream_t)stream,
-                     (const Params*)h->dprm, (int)B, io);
-  if (h->kernE)
-    hipLaunchKernelGGL(h->kernE, dim3(B), dim3(WAVE), h->lds_bytesE, (hipStream_t)stream,
+  IO ioE;
+  Run run;
+  if (int rc = eq_prepare(h, B, io, ioE, (hipStream_t)stream, host_eq, &run)) return rc;
+  if (run.A)
+    hipLaunchKernelGGL(h->kern, dim3(B), dim3(WAVE), h->lds_bytes, (hipStream_t)stream,
                        (const Params*)h->dprm, (int)B, io);
+  if (run.E)
+    hipLaunchKernelGGL(h->kernE, dim3(B), dim3(WAVE), h->lds_bytesE, (hipStream_t)stream,
+                       (const Params*)h->dprm, (int)B, ioE);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return fail(NMPC_E_HIP, std::string("kernel launch: ") + hipGetErrorString(e));
   return NMPC_OK;
+}
+
+int nmpc_solve_batch_dev(nmpc_handle* h, int32_t B, const double* x0, int64_t ld_x0, const double* lbx,
+                         int64_t ld_lbx, const double* ubx, int64_t ld_ubx, const double* lbg, int64_t ld_lbg,
+                         const double* ubg, int64_t ld_ubg, const double* p, int64_t ld_p, double* x_out,
+                         double* f_out, double* g_out, double* lam_x_out, double* lam_g_out, double* lam_p_out,
+                         double* X_out, int32_t* status, int32_t* iters, void* stream) {
+  return solve_dev(h, B, x0, ld_x0, lbx, ld_lbx, ubx, ld_ubx, lbg, ld_lbg, ubg, ld_ubg, p, ld_p, x_out, f_out, g_out,
+                   lam_x_out, lam_g_out, lam_p_out, X_out, status, iters, stream, -1);
 }
 
 int nmpc_solve_batch(nmpc_handle* h, int32_t B, const double* x0, int64_t ld_x0, const double* lbx, int64_t ld_lbx,
@@ -4853,9 +4993,11 @@ int nmpc_solve_batch(nmpc_handle* h, int32_t B, const double* x0, int64_t ld_x0,
   up(d_x0, x0, n_x0); up(d_lbx, lbx, n_lbx); up(d_ubx, ubx, n_ubx);
   up(d_lbg, lbg, n_lbg); up(d_ubg, ubg, n_ubg); up(d_p, p, n_p);
   if (e != hipSuccess) return fail(NMPC_E_HIP, std::string("hipMemcpy H2D: ") + hipGetErrorString(e));
-  int rc = nmpc_solve_batch_dev(h, B, d_x0, ld_x0, d_lbx, ld_lbx, d_ubx, ld_ubx, d_lbg, ld_lbg, d_ubg, ld_ubg,
-                                d_p, ld_p, d_x, d_f, d_g, d_lx, d_lg, lam_p_out ? d_lp : nullptr, d_X, d_st, d_it,
-                                nullptr);
+  // the bounds are on the host here: the equality-row test costs no device round trip
+  const int heq = h->kernE ? host_has_eq(B, (int)ng, lbg, ld_lbg, ubg, ld_ubg) : 0;
+  int rc = solve_dev(h, B, d_x0, ld_x0, d_lbx, ld_lbx, d_ubx, ld_ubx, d_lbg, ld_lbg, d_ubg, ld_ubg,
+                     d_p, ld_p, d_x, d_f, d_g, d_lx, d_lg, lam_p_out ? d_lp : nullptr, d_X, d_st, d_it,
+                     nullptr, heq);
   if (rc != NMPC_OK) return rc;
   e = hipDeviceSynchronize();
   if (e != hipSuccess) return fail(NMPC_E_HIP, std::string("kernel: ") + hipGetErrorString(e));
@@ -4910,10 +5052,9 @@ int nmpc_closed_loop_dev(nmpc_handle* h, int32_t B, int32_t K, const double* lbx
   io.ld_lbx = ld_lbx; io.ld_ubx = ld_ubx; io.ld_lbg = ld_lbg; io.ld_ubg = ld_ubg;
   if (int rc = ensure_ws(h, B)) return rc;
   io.ws = h->dws;
-  io.eqflag = h->kernE ? h->deq : nullptr;
-  if (h->kernE) {
-    if (int rc = eq_gate(h, B, io, (hipStream_t)stream)) return rc;
-  }
+  IO ioE;
+  Run run;
+  if (int rc = eq_prepare(h, B, io, ioE, (hipStream_t)stream, -1, &run)) return rc;
   Loop lp;
   lp.K = K; lp.p = p; lp.ld_p = ld_p; lp.w = w; lp.vt = v_t; lp.wt = w_t; lp.ld_tk = ld_tk; lp.ld_tb = ld_tb;
   lp.u_hist = u_hist; lp.x_hist = x_hist; lp.f_hist = f_hist; lp.fov_hist = fov_hist;
@@ -5000,19 +5141,20 @@ int nmpc_closed_loop_dev(nmpc_handle* h, int32_t B, int32_t K, const double* lbx
       const int w = std::atoi(ev);
       if (w >= NXCD && w < waves) waves = w;
     }
-    hipLaunchKernelGGL(h->sched, dim3(waves), dim3(WAVE), h->lds_bytes, (hipStream_t)stream,
-                       (const Params*)h->dprm, (int)B, io, lp, q);
-    // the equality class on the same queues (exactly one of the pair runs); when its own
-    // occupancy cannot put a wave on every XCD, one workgroup per scenario instead, on the
-    // same completion-guard state (zeroed by nmpc_sched_init_kernel)
-    if (h->schedE && h->residentE >= NXCD) {
+    if (run.A)
+      hipLaunchKernelGGL(h->sched, dim3(waves), dim3(WAVE), h->lds_bytes, (hipStream_t)stream,
+                         (const Params*)h->dprm, (int)B, io, lp, q);
+    // the equality class on the same queues (when paired, exactly one of the pair runs);
+    // when its own occupancy cannot put a wave on every XCD, one workgroup per scenario
+    // instead, on the same completion-guard state (zeroed by nmpc_sched_init_kernel)
+    if (run.E && h->residentE >= NXCD) {
       hipLaunchKernelGGL(h->schedE, dim3(h->residentE < waves ? h->residentE : waves), dim3(WAVE), h->lds_bytesE,
-                         (hipStream_t)stream, (const Params*)h->dprm, (int)B, io, lp, q);
-    } else if (h->loopE) {
+                         (hipStream_t)stream, (const Params*)h->dprm, (int)B, ioE, lp, q);
+    } else if (run.E) {
       Loop lpE = lp;
       lpE.done = q.done;
       hipLaunchKernelGGL(h->loopE, dim3(B), dim3(WAVE), h->lds_bytesE, (hipStream_t)stream,
-                         (const Params*)h->dprm, (int)B, io, lpE);
+                         (const Params*)h->dprm, (int)B, ioE, lpE);
     }
     h->last_policy = 1;
     h->last_waves = waves;
@@ -5022,11 +5164,12 @@ int nmpc_closed_loop_dev(nmpc_handle* h, int32_t B, int32_t K, const double* lbx
     lp.done = q.done;
     hipLaunchKernelGGL(nmpc_guard_init_kernel, dim3((B + thr - 1) / thr), dim3(thr), 0, (hipStream_t)stream,
                        (int)B, q);
-    hipLaunchKernelGGL(h->loop, dim3(B), dim3(WAVE), h->lds_bytes, (hipStream_t)stream,
-                       (const Params*)h->dprm, (int)B, io, lp);
-    if (h->loopE)
-      hipLaunchKernelGGL(h->loopE, dim3(B), dim3(WAVE), h->lds_bytesE, (hipStream_t)stream,
+    if (run.A)
+      hipLaunchKernelGGL(h->loop, dim3(B), dim3(WAVE), h->lds_bytes, (hipStream_t)stream,
                          (const Params*)h->dprm, (int)B, io, lp);
+    if (run.E)
+      hipLaunchKernelGGL(h->loopE, dim3(B), dim3(WAVE), h->lds_bytesE, (hipStream_t)stream,
+                         (const Params*)h->dprm, (int)B, ioE, lp);
   }
   // completion guard, both policies: every scenario ran its K steps, else err |= 2 and
   // the unrun steps are marked in the histories

@@ -24,7 +24,7 @@ EXPORTS = (
     "nmpc_default_options", "nmpc_create", "nmpc_destroy", "nmpc_dims",
     "nmpc_solve_batch", "nmpc_solve_batch_dev", "nmpc_set_trace", "nmpc_read_trace",
     "nmpc_shift_dev", "nmpc_closed_loop_dev", "nmpc_closed_loop_info", "nmpc_last_error", "nmpc_kernel_info",
-    "nmpc_build_id", "nmpc_closed_loop_times",
+    "nmpc_build_id", "nmpc_closed_loop_times", "nmpc_memory_info",
 )
 
 _OPT_INT = ("max_iter", "acceptable_iter", "max_soc", "max_soft_resto_iters",
@@ -105,6 +105,7 @@ def lib():
     L.nmpc_build_id.argtypes = []
     L.nmpc_build_id.restype = C.c_char_p
     L.nmpc_kernel_info.argtypes = [vp, i32p, i32p]
+    L.nmpc_memory_info.argtypes = [vp] + [C.POINTER(C.c_int64)] * 4
     L.nmpc_closed_loop_info.argtypes = [vp, i32p, i32p, i32p, i32p, C.POINTER(C.c_int64)]
     for n in EXPORTS:
         if n not in ("nmpc_default_options", "nmpc_last_error", "nmpc_build_id"):

@@ -366,6 +366,13 @@ class Solver:
         _lib.check(_lib.lib().nmpc_kernel_info(self._h, C.byref(lds), C.byref(tps)))
         return {"lds_bytes": lds.value, "threads_per_scenario": tps.value}
 
+    def memory_info(self):
+        """Device workspace the handle holds: the problem class's, and the equality class's
+        (allocated only once a batch with equality rows was solved); per-scenario sizes."""
+        v = [C.c_int64() for _ in range(4)]
+        _lib.check(_lib.lib().nmpc_memory_info(self._h, *[C.byref(x) for x in v]))
+        return dict(zip(("ws_bytes", "ws_eq_bytes", "ws_per_scenario", "ws_eq_per_scenario"), (x.value for x in v)))
+
     def stats(self) -> dict:
         return dict(self._stats)
 

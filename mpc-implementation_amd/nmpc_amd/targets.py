@@ -35,6 +35,8 @@ SCHEDULES = {
     # shift1.m expects the target)
     "matlab_nmpc_tt": [(0, 15.0, 0.12)],
     "dynamic_obstacles": [(0, 15.0, 0.12)],
+    # the derived start of that script's problem (tests/golden/gen_reference_runs.py)
+    "dynamic_obstacles_derived": [(0, 15.0, 0.12)],
     # Python/T_Trajectory.py:25-57
     "t_trajectory": [
         (0, 13.5, 0.0), (100, 13.5, (PI / 2) / 12), (160, 13.5, 0.0), (260, 13.5, -(PI / 2) / 12),

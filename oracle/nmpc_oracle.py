@@ -951,8 +951,11 @@ class IpoptDense:
                         if ok and all(phi_o <= fp or th_o <= ft for fp, ft in ofilt):
                             break
                 # ---- the restoration NLP's own termination
-                err_r, dinf_r, cv_r, cm_r, _, _, _ = errR(xx, ss, dR, JR, pp, nn, yR, zlR, zuR, vlR, vuR, zp, zn,
-                                                          muR, 0.0)
+                err_r, dinf_r, cv_r, cm_r, sd_r, sc_r, _ = errR(xx, ss, dR, JR, pp, nn, yR, zlR, zuR, vlR, vuR, zp,
+                                                                zn, muR, 0.0)
+                if trace_:  # the restoration NLP's own check (the kernel's trace: negative error)
+                    self.chk.append(dict(it=it_, err=err_r, dinf=dinf_r / sd_r, cviol=cv_r, cmp=cm_r / sc_r,
+                                         resto=True))
                 if not np.isfinite(err_r):
                     return dict(status=INVALID_NUMBER_DETECTED, it=it_, x=xx)
                 conv = (err_r <= o["tol"] and dinf_r <= o["dual_inf_tol"] and cv_r <= o["constr_viol_tol"]

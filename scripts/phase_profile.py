@@ -19,7 +19,7 @@ t = time.time()
 s(x0=np.zeros(spec.nw), lbx=lbx, ubx=ubx, lbg=lbg, ubg=ubg, p=P.T)
 print("wall", time.time() - t)
 tr = s.read_trace(B)
-st = tr[:, s.max_iter:, :].reshape(B, -1)[:, :24]
+st = tr[:, s.max_iter + 1:, :].reshape(B, -1)[:, :24]
 it = s.stats()["iter_count"]
 tot = st[:, 15].mean()
 print(f"B={B} mean iters {np.mean(it):.2f}; mean total cycles/scenario {tot:.3e} ({tot/np.mean(it):.3e} per iter)")

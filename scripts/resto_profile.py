@@ -20,7 +20,7 @@ for _ in range(2):
     s(x0=W.T, lbx=lbx, ubx=ubx, lbg=lbg, ubg=ubg, p=Pm.T)
     wall = time.time() - t
 tr = s.read_trace(B)
-st = tr[:, s.max_iter:, :].reshape(B, -1)[:, :24]
+st = tr[:, s.max_iter + 1:, :].reshape(B, -1)[:, :24]
 it = s.stats()["iter_count"]
 tot = st[:, 15]
 print(f"B={B} wall {wall*1e3:.1f} ms; iters mean {np.mean(it):.1f} max {np.max(it)}; "

@@ -34,6 +34,9 @@ for rep in range(2):
     torch.cuda.synchronize()
 t = s.closed_loop_times(B, K).astype(np.int64)
 it = h["iters"].cpu().numpy()
+if len(sys.argv) > 1:  # raw record for offline analysis (scripts/sched_sim.py)
+    np.savez_compressed(sys.argv[1], times=t, iters=it, status=h["status"].cpu().numpy(),
+                        order=order.cpu().numpy())
 st, en = t[:, :, 0], t[:, :, 1]
 t0 = st.min()
 span = (en.max() - t0) / 1e5  # ms (100 MHz)

@@ -51,6 +51,19 @@ Round 4 adds the two MATLAB runs that define BASELINE configs 1 and 5:
                      step with con_t = [15; 0.12] (shift1.m:8-12) every step; sc (the step
                      counter) selects nothing.
 
+Round 5 adds one DERIVED run (not a run the reference performs):
+
+  dynamic_obstacles_derived  Dynamic Obstacle avoidance.m with everything the script fixes
+                     kept -- its obstacle table (:98-119), the y_o windows (:213-230), its
+                     literal bounds (:156-178), T, N and con_t = [15; 0.12] (shift1.m:9) --
+                     except the start: the UAV at (-61, 150, 80) and the target at
+                     (-60, 150), heading +x, inside the obstacle corridor, 600 steps.  The
+                     target then circles (radius 15 / 0.12 = 125 m) around (-60, 275), a path
+                     that passes within ~60 m of obstacle 2 at x = 0 while that obstacle's y
+                     moves from 300 to 1 (steps 101..399), so its moving row is active: the
+                     script's own start at x = -501 never comes within 370 m of a moving
+                     obstacle, which leaves the moving rows unexercised.  Labelled derived.
+
 Solvers (`--solver`):
   numpy  oracle/nmpc_oracle.py IpoptDense (dense single-shooting IPOPT
          restatement) -- the committed fixtures (ref_run_<name>.npz);
@@ -86,6 +99,8 @@ X0_MATLAB_NG = [90.0, 150.0, 80.0, 0.0, 0.0]                 # MATLAB/Dynamic Ob
 X0_DYNAMIC = [-501.0, 150.0, 80.0, 0.0, 0.0, 0.0, 0.0, 0.0]  # Dynamic Obstacle avoidance.m:183
 XS0_DYNAMIC = [-500.0, 150.0, 0.0]                           # Dynamic Obstacle avoidance.m:184
 Y_OBS0_DYNAMIC = [0.0, 300.0, 0.0, 300.0, 0.0, 300.0]        # Dynamic Obstacle avoidance.m:98-109 (y_o_1..6)
+X0_DYNAMIC_DERIVED = [-61.0, 150.0, 80.0, 0.0, 0.0, 0.0, 0.0, 0.0]  # derived start, inside the corridor
+XS0_DYNAMIC_DERIVED = [-60.0, 150.0, 0.0]
 
 RUNS = {
     "nmpc_tt": dict(layout="nmpc_tt", N=15, T=1.0, x0=X0_NMPC_TT, K=700),
@@ -94,6 +109,10 @@ RUNS = {
     "matlab_nmpc_tt": dict(layout=None, N=15, T=0.2, x0=X0_MATLAB_NG, K=100, model="uav5"),
     "dynamic_obstacles": dict(layout="dynamic", N=15, T=0.2, x0=X0_DYNAMIC, xs=XS0_DYNAMIC, K=1500,
                               dynamic=True),
+    # derived (see the module docstring): the script's problem from a start inside the corridor
+    "dynamic_obstacles_derived": dict(layout="dynamic", N=15, T=0.2, x0=X0_DYNAMIC_DERIVED,
+                                      xs=XS0_DYNAMIC_DERIVED, K=600, dynamic=True, derived=True,
+                                      bounds_of="dynamic_obstacles", schedule_of="dynamic_obstacles"),
 }
 
 
@@ -193,7 +212,7 @@ def run(name, solver="numpy", K=None, log_every=100):
     c = RUNS[name]
     K = K or c["K"]
     prob = run_problem(name)
-    lbx, ubx, lbg, ubg = literal_bounds(name, c["N"])
+    lbx, ubx, lbg, ubg = literal_bounds(c.get("bounds_of", name), c["N"])
     if solver.startswith("numpy"):
         ipo = orc.IpoptDense(prob, orc.REFERENCE_OPTS, la_variant=int(solver[5:] or 0))
 
@@ -217,7 +236,7 @@ def run(name, solver="numpy", K=None, log_every=100):
         p = np.concatenate([x0, xs, yobs])   # args.p = [x0; xs (; y_o_1..6)]
         st, ni, x, f = solve(w, p)
         U = x.reshape(N, nu).T   # ca.reshape(sol['x'], nu, N)
-        x1, _, xs1 = orc.shift_timestep(prob, x0, U, xs, con_t=con_t(name, it))
+        x1, _, xs1 = orc.shift_timestep(prob, x0, U, xs, con_t=con_t(c.get("schedule_of", name), it))
         rec["p"].append(p); rec["status"].append(st); rec["iter"].append(ni)
         rec["x"].append(x.copy()); rec["f"].append(f)
         rec["fov"].append(fov_error(name, x1, xs))

@@ -31,6 +31,10 @@ Two measurements per run, written to ref_run_<name>_spread.npz:
     python tests/golden/gen_rounding_spread.py [<run>|all] [--jobs 8]
     python tests/golden/gen_rounding_spread.py --add-cpp-steps [<run>|all]
         (adds the compiled restatement's per-step row to existing spread files)
+    python tests/golden/gen_rounding_spread.py --add-step-x [<run>|all] [--jobs 8]
+        (adds, for every rounding-sensitive step -- a step whose status, iterations, x or f
+        some variant moves -- each variant's status and x: env_steps, env_status, env_x,
+        the per-step envelope tests/test_gpu_reference_runs.py holds the GPU's result to)
 """
 import argparse
 import multiprocessing as mp
@@ -118,6 +122,62 @@ def add_cpp_steps(names):
               f"{int((it != z['iter']).sum())}, conv x>1e-6 {int((conv & (st == z['status']) & (dx > 1e-6)).sum())}")
 
 
+def sensitive_steps(z, sp, tol=1e-6):
+    """The test's definition (tests/test_gpu_reference_runs.py::_sensitive)."""
+    st, it = sp["step_status"], sp["step_iter"]
+    return np.flatnonzero((st != z["status"]).any(0) | (it != z["iter"]).any(0)
+                          | (sp["step_dev_x"] > tol).any(0) | (sp["step_dev_f"] > tol).any(0))
+
+
+def step_x_job(args):
+    name, v, steps = args
+    from threadpoolctl import threadpool_limits
+    from oracle import nmpc_oracle as orc
+
+    threadpool_limits(1)
+    z = _fixture(name)
+    W = warm_starts(name, z)
+    ipo = orc.IpoptDense(grr.run_problem(name), orc.REFERENCE_OPTS, la_variant=v)
+    out = []
+    for k in steps:
+        r = ipo.solve(W[k], z["lbx"], z["ubx"], z["lbg"], z["ubg"], z["p"][k])
+        out.append((int(k), int(r["status"]), np.asarray(r["x"], float)))
+    return name, v, out
+
+
+def add_step_x(names, jobs):
+    from oracle import nmpc_oracle as orc, cpu_ipopt
+    todo = {}
+    for n in names:
+        z, sp = _fixture(n), dict(np.load(os.path.join(HERE, f"ref_run_{n}_spread.npz")))
+        todo[n] = (z, sp, sensitive_steps(z, sp))
+    jobs_l = [(n, v, list(todo[n][2][i:i + 20])) for n in names for v in VARIANTS
+              for i in range(0, len(todo[n][2]), 20)]
+    res = {n: {v: {} for v in VARIANTS} for n in names}
+    with mp.get_context("fork").Pool(jobs) as pool:
+        for n, v, out in pool.imap_unordered(step_x_job, jobs_l):
+            for k, st, x in out:
+                res[n][v][k] = (st, x)
+    for n in names:
+        z, sp, steps = todo[n]
+        nw = z["x"].shape[1]
+        W = warm_starts(n, z)
+        c = cpu_ipopt.solve_batch(grr.run_problem(n), W[steps], z["p"][steps], z["lbx"], z["ubx"], z["lbg"],
+                                  z["ubg"], orc.REFERENCE_OPTS, threads=8) if len(steps) else None
+        ns = len(VARIANTS) + 1
+        est = np.zeros((ns, len(steps)), np.int16)
+        ex = np.zeros((ns, len(steps), nw))
+        for j, k in enumerate(steps):
+            for i, v in enumerate(VARIANTS):
+                est[i, j], ex[i, j] = res[n][v][int(k)]
+            est[-1, j], ex[-1, j] = c["status"][j], c["x"][j]
+        # the per-step rows of the same solvers must agree with what was measured before
+        assert np.array_equal(est, sp["step_status"][:, steps]), n
+        sp.update(env_steps=steps.astype(np.int32), env_status=est, env_x=ex)
+        np.savez_compressed(os.path.join(HERE, f"ref_run_{n}_spread.npz"), **sp)
+        print(f"{n}: {len(steps)} rounding-sensitive steps, each variant's status and x stored", flush=True)
+
+
 def whole_job(args):
     name, solver = args
     z = _fixture(name)
@@ -133,10 +193,14 @@ def main():
     ap.add_argument("run", nargs="?", default="all")
     ap.add_argument("--jobs", type=int, default=8)
     ap.add_argument("--add-cpp-steps", action="store_true")
+    ap.add_argument("--add-step-x", action="store_true")
     a = ap.parse_args()
     names = list(grr.RUNS) if a.run == "all" else [a.run]
     if a.add_cpp_steps:
         add_cpp_steps(names)
+        return
+    if a.add_step_x:
+        add_step_x(names, a.jobs)
         return
     jobs_w = [(n, s) for n in names for s in WHOLE]
     jobs_w.sort(key=lambda j: -grr.RUNS[j[0]]["K"] * (0.05 if j[1] == "cpp" else 1.0))

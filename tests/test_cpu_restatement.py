@@ -225,19 +225,19 @@ def test_fixed_variables_against_oracle(cpu, model):
             assert np.max(np.abs(r["x"][b] - o["x"]) / (1 + np.abs(o["x"]))) <= TOL
 
 
-@pytest.mark.parametrize("name", ["nmpc_tt", "10_obstacles", "race_track_2"])
+@pytest.mark.parametrize("name", ["nmpc_tt", "10_obstacles", "race_track_2", "dynamic_obstacles_derived"])
 def test_reference_run_fixture_per_step(cpu, name):
     """The reference scripts' own runs (tests/golden/gen_reference_runs.py: NMPC_TT.py 700
     steps, 10_obstacles.py 1,595, Race Track 2.py 2,000; the numpy oracle's loop): every
     step re-solved by the compiled restatement from the oracle's exact (w, p), with the
     scripts' literal N = 15 bound vectors."""
     from oracle import nmpc_oracle as orc
-    from gen_reference_runs import RUNS, warm_start, literal_bounds
+    from gen_reference_runs import RUNS, warm_start, literal_bounds, run_problem
 
     z = np.load(os.path.join(GOLD, f"ref_run_{name}.npz"))
     c = RUNS[name]
-    prob = orc.make_problem(c["layout"], N=c["N"], T=c["T"])
-    lb = literal_bounds(name, c["N"])
+    prob = run_problem(name)
+    lb = literal_bounds(c.get("bounds_of", name), c["N"])
     for a, b in zip(lb, (z["lbx"], z["ubx"], z["lbg"], z["ubg"])):
         np.testing.assert_array_equal(a, b)
     K = len(z["status"])
@@ -260,7 +260,10 @@ def test_reference_run_fixture_per_step(cpu, name):
     # a converged step whose termination test fell one iteration apart (rounding) stops at
     # a different point of the tol = 1e-8 neighbourhood: on the flat directions of these
     # costs x can then differ by more than 1e-6 while f agrees to ~1e-10
-    assert same.mean() >= 0.99
+    # the derived run drives an obstacle into the UAV (steps 258..304: clearance < 0): there
+    # max_iter / restoration-failure / infeasibility decisions part at the rounding level,
+    # converged steps still agree
+    assert same.mean() >= (0.98 if RUNS[name].get("derived") else 0.99)
     assert ok_f.sum() >= conv.sum() - 1
     assert ok_x.sum() >= 0.97 * conv.sum()
     assert (r["iter"] == z["iter"]).mean() >= 0.95
@@ -276,3 +279,35 @@ def test_reference_run_literal_bounds_match_spec():
         got = make_spec(layout, N=15, T=0.2).bounds()
         for a, b in zip(literal_bounds(name), got):
             np.testing.assert_array_equal(a, b)
+
+
+def test_derived_dynamic_run_exercises_the_moving_rows():
+    """The derived run (gen_reference_runs.py: Dynamic Obstacle avoidance.m's problem from a
+    start inside the obstacle corridor) brings the UAV within the horizon's reach of a
+    MOVING obstacle -- minimum clearance of the plant state below 90 m on many steps, where
+    the script's own start keeps >= 373 m -- so the moving rows shape the solutions: on
+    converged steps a moving-obstacle row comes within 10 m of its bound, and where the
+    obstacle runs into the UAV (clearance < 0) the rows are violated and the solver works
+    on them in restoration (max_iter / infeasible / restoration-failure steps)."""
+    from oracle import nmpc_oracle as orc
+    from gen_reference_runs import run_problem
+
+    z = np.load(os.path.join(GOLD, "ref_run_dynamic_obstacles_derived.npz"))
+    prob = run_problem("dynamic_obstacles_derived")
+    P = z["p"]
+    ox, r = np.asarray(prob.obs_x, float), np.asarray(prob.obs_rsum, float)
+    oy = np.tile(np.asarray(prob.obs_y, float), (len(P), 1))
+    oy[:, :6] = P[:, 11:17]               # the moving obstacles' y (p[11:17])
+    clear = np.hypot(P[:, :1] - ox, P[:, 1:2] - oy) - r
+    moving = clear[:, :6].min(1)
+    near = viol = 0
+    for k in range(len(P)):
+        g = orc.constraints(prob, z["x"][k], P[k]).reshape(prob.N + 1, prob.m)[:, 5:11].max()
+        near += bool(z["status"][k] in (0, 1) and g >= -10.0)
+        viol += bool(z["status"][k] not in (0, 1) and g > 0.0)
+    print(f"\nderived run: min clearance to a moving obstacle {moving.min():.2f} m; steps within 90 m "
+          f"{(moving < 90).sum()}/{len(P)}; converged steps with a moving row within 10 m of its bound {near}; "
+          f"unconverged steps with a moving row violated {viol}; statuses "
+          f"{dict(zip(*np.unique(z['status'], return_counts=True)))}")
+    assert moving.min() < 90 and (moving < 90).sum() >= 50
+    assert near >= 20 and viol >= 1

@@ -82,12 +82,15 @@ def test_two_rank_fused_gather_equals_single_rank():
 
 @pytest.mark.timeout(600)
 def test_config4_eight_rank_bench_rehearsal_equals_single_rank():
-    """BASELINE config 4's global batch through bench.py's own multi-rank fused path:
-    32,768 scenarios sharded 4,096 per rank over 8 ranks (torch.distributed.run, gloo
-    backend via NMPC_BENCH_BACKEND, every rank on cuda:0 of this one-GPU box), W = 1
-    warm-up step, K = 2 timed closed-loop steps, then the fused mode's single
-    all-gather.  Rank 0's gathered rows must equal one single-rank bench run over all
-    32,768 scenarios bitwise (results do not depend on the GPU count)."""
+    """BASELINE config 4's global batch through bench.py's own multi-rank fused path,
+    started exactly as the driver starts it -- `python bench.py --gpus 8 ...` with no
+    launcher around it: bench.py starts its 8 ranks itself (torch.distributed.run as a
+    child process), 32,768 scenarios sharded 4,096 per rank (gloo backend via
+    NMPC_BENCH_BACKEND, every rank on cuda:0 of this one-GPU box), W = 1 warm-up step,
+    K = 2 timed closed-loop steps, then the fused mode's single all-gather.  The relayed
+    line must say 8 GPUs and 32,768 scenarios, and rank 0's gathered rows must equal one
+    single-rank bench run over all 32,768 scenarios bitwise (results do not
+    depend on the GPU count)."""
     import subprocess
     import sys
 
@@ -95,17 +98,18 @@ def test_config4_eight_rank_bench_rehearsal_equals_single_rank():
     os.makedirs(out, exist_ok=True)
     multi, single = os.path.join(out, "cfg4_rows_8rank.npy"), os.path.join(out, "cfg4_rows_1rank.npy")
     common = ["--steps", "2", "--warmup", "1", "--no-per-step", "--no-cpu-baseline"]
-    env = dict(os.environ, NMPC_BENCH_BACKEND="gloo", OMP_NUM_THREADS="2")
-    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "8",
-                        "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
-                        os.path.join(ROOT, "bench.py"), "--gpus", "8", "--batch", "4096", *common,
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(NMPC_BENCH_BACKEND="gloo", OMP_NUM_THREADS="2")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "8", "--batch", "4096", *common,
                         "--dump-rows", multi], cwd=ROOT, env=env, capture_output=True, text=True, timeout=540)
     print(r.stdout[-2000:], r.stderr[-3000:])
     assert r.returncode == 0
+    assert r.stdout.strip().splitlines()[-1].startswith("{")  # the relayed line is the last stdout line
     line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1]
     import json
     res = json.loads(line)
     assert res["n_gpus"] == 8 and res["config"]["global_batch"] == 32768
+    assert res["config"]["parallelism"] == "dp8" and res["steps"] == 2
     r1 = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--batch", "32768", *common,
                          "--dump-rows", single], cwd=ROOT, capture_output=True, text=True, timeout=300)
     print(r1.stdout[-1000:], r1.stderr[-2000:])

@@ -218,3 +218,58 @@ def test_watchdog_stop_with_equality_rows_matches_oracle(case, last, skip):
           f"GPU status {int(np.ravel(st['status_code'])[0])} / {int(np.ravel(st['iter_count'])[0])} iterations, "
           f"oracle {ref['status']} / {ref['iter']}; mismatches {bad}")
     assert not bad
+
+
+def test_equality_workspace_is_allocated_lazily():
+    """The equality class's workspace (~840 KB per scenario: global rows up to N = 63 and the
+    128 x 128 Schur storage) is allocated only once a batch with equality rows is solved; a
+    config-3 handle whose batches have none holds its class's ~120 KB per scenario only.
+    Device-pointer batches: without the equality workspace the bounds are scanned and the
+    applicable class launched alone; once it exists, the gated pair runs -- the results are
+    bitwise the same either way, and an equality batch through the device path equals the
+    host path's solve of it."""
+    import torch
+    from nmpc_amd import nlpsol, config_spec, draw_scenarios, make_spec, REFERENCE_OPTS
+
+    f64 = dict(dtype=torch.float64, device="cuda")
+    spec = config_spec(3)
+    s3 = nlpsol("solver", "ipopt", spec, REFERENCE_OPTS)
+    B = 256
+    P = draw_scenarios(spec, B, seed=1003)
+    bnd = [torch.tensor(v, **f64) for v in spec.bounds()]
+    hist = {"status": torch.empty(2, B, dtype=torch.int32, device="cuda")}
+    s3.closed_loop_device(2, *bnd, torch.tensor(P, **f64), torch.zeros(B, spec.nw, **f64),
+                          torch.full((B,), 12.0, **f64), torch.full((B,), 0.01, **f64), hist)
+    torch.cuda.synchronize()
+    mi = s3.memory_info()
+    print(mi)
+    assert mi["ws_eq_bytes"] == 0 and mi["ws_bytes"] == B * mi["ws_per_scenario"]
+    assert mi["ws_per_scenario"] <= 130_000 < mi["ws_eq_per_scenario"]
+
+    prob, p, lbx, ubx, lbg, ubg, row = _pinned_z_problem(0)
+    s = nlpsol("solver", "ipopt", make_spec("race_track_2", N=8, T=0.2), REFERENCE_OPTS)
+    Bs = 3
+    pd = torch.tensor(np.tile(p, (Bs, 1)), **f64)
+    x0 = torch.zeros(Bs, prob.nw, **f64)
+
+    def dev_solve(lg, ug):
+        out = {"x": torch.empty(Bs, prob.nw, **f64), "f": torch.empty(Bs, **f64),
+               "status": torch.empty(Bs, dtype=torch.int32, device="cuda"),
+               "iters": torch.empty(Bs, dtype=torch.int32, device="cuda")}
+        b = [torch.tensor(v, **f64) for v in (lbx, ubx, lg, ug)]
+        s.solve_device(x0, *b, pd, out)
+        torch.cuda.synchronize()
+        return {k: v.cpu().numpy() for k, v in out.items()}
+
+    lbg0, ubg0 = orc.bounds(prob)[2:]
+    a1 = dev_solve(lbg0, ubg0)                      # no equality row: the class alone
+    assert s.memory_info()["ws_eq_bytes"] == 0
+    e1 = dev_solve(lbg, ubg)                        # equality rows: the equality class, workspace now
+    assert s.memory_info()["ws_eq_bytes"] == Bs * s.memory_info()["ws_eq_per_scenario"]
+    a2 = dev_solve(lbg0, ubg0)                      # the gated pair, decided on the device
+    for k in a1:
+        np.testing.assert_array_equal(a1[k], a2[k])
+    h = s(x0=np.zeros(prob.nw), lbx=lbx, ubx=ubx, lbg=lbg, ubg=ubg, p=p)
+    assert int(e1["status"][0]) == int(np.ravel(s.stats()["status_code"])[0]) == orc.SOLVE_SUCCEEDED
+    np.testing.assert_array_equal(e1["x"][0], h["x"].ravel())
+    assert abs(float(h["g"].ravel()[row]) - lbg[row]) <= 1e-6
