@@ -654,6 +654,11 @@ struct Solver {
   // --------------------------------------------- stage derivatives at X (lanef()=k)
   // gl[k] = grad l_k (8), Hl[k] = hess l_k packed over (x,y,z,x5,x6,x7), trig[k].
   // Derivation: oracle/nmpc_oracle.py::stage_cost_derivs (Q = (r1/a)^2+(r2/b)^2).
+  // HESS = false: trig and the gradient only -- the restoration phase weights the original
+  // objective by 0 (hfac = 0 in its assembly, so Hl is never read there; its 0 * gl terms
+  // keep the gradient's exact values); the full derivatives are formed again when it
+  // returns to the original problem
+  template <bool HESS = true>
   __device__ __forceinline__ void derivs(const LDS double* Xs, const GLB double* Us) {
     STAMP0();
     const int k = lanef();
@@ -667,7 +672,8 @@ struct Solver {
       GLB double* H = Hl + k * 21;
       if (k == N) {
         for (int i = 0; i < 8; ++i) g8[i] = 0.0;
-        for (int i = 0; i < 21; ++i) H[i] = 0.0;
+        if (HESS)
+          for (int i = 0; i < 21; ++i) H[i] = 0.0;
       } else {
         const double hv = P->hv, hh = P->hh;
         const double x = xk[0], yy = xk[1], z = xk[2], x5 = xk[5], x6 = xk[6], x7 = xk[7];
@@ -719,7 +725,7 @@ struct Solver {
         g8[5] = g6[3]; g8[6] = g6[4]; g8[7] = g6[5];
         // Hessian, 21 packed entries
 #pragma unroll
-        for (int qa = 0; qa < 6; ++qa) {
+        for (int qa = 0; qa < (HESS ? 6 : 0); ++qa) {
 #pragma unroll
           for (int qb = qa; qb < 6; ++qb) {
             // sparse second derivatives of ex, ey, a, b
@@ -2830,7 +2836,7 @@ __device__ __forceinline__ void resto_phase(const Params* __restrict__ prm, doub
           sync();
           S.rollout(S.U, S.X);
           V[12] = S.df * S.eval_fg(S.X, S.d, S.dc);
-          S.derivs(S.X, S.U);
+          S.template derivs<false>(S.X, S.U);
           V[15] = WD[0]; V[16] = WD[1]; V[17] = WD[2]; V[23] = 0.0;
           S.delta = WD[5];
           rwd_dir = true;
@@ -2997,7 +3003,7 @@ __device__ __forceinline__ void resto_phase(const Params* __restrict__ prm, doub
           sync();
           V[12] = V[20];
           STAMP1(PH_ACCEPT);
-          S.derivs(S.X, S.U);
+          S.template derivs<false>(S.X, S.U);
           ++it;
           if (trace && S.lanef() == 0) {
             double th = 0.0;
@@ -3016,6 +3022,9 @@ __device__ __forceinline__ void resto_phase(const Params* __restrict__ prm, doub
       io.status = rstat;
       io.it = it;
       if (rstat != 0) return;
+      // back to the original problem: its objective's Hessian at the current iterate (the
+      // restoration iterations formed the gradient only)
+      S.derivs(S.X, S.U);
       // ---- back to the original problem: bound multipliers by a Newton step for
       //      complementarity over the whole restoration (fraction to the boundary,
       //      reset to 1 above bound_mult_reset_threshold); y = 0 (constr_mult_reset_threshold)
