@@ -651,6 +651,103 @@ struct Solver {
     return fs;
   }
 
+  // ------------------------------------ two line-search trials' stage work at once
+  // The restoration line search's next backtracking trial (a1 = a0 * alpha_red_factor) has
+  // its rollout and row values formed together with the current one's (a0): the stage-
+  // parallel work uses N + 1 of 64 lanes, so lanes 32 + k carry stage k of the second trial
+  // in the same instructions.  Group 0 (lanes 0..31) writes Xt / dt and its increments to
+  // `inc` exactly as rollout / eval_fg do; group 1 writes its X to `lam`, its row values to
+  // `dms` and its increments to `qs` (all three dead during a line search: lam is re-formed
+  // by the next adjoint, qs by the next assembly, dms is the main phase's scratch).  Every
+  // stage's arithmetic is that of rollout / eval_fg, and the objective's wave sum of group 1
+  // sits in lanes 32..63 -- the butterfly reduces each 32-lane half in the same order, so
+  // both objectives are bitwise those of two separate calls.
+  static constexpr bool kSpec = CAP::lds_rows && !CAP::refine && !CAP::eq && CAP::nmax <= 31;
+  __device__ __forceinline__ void rollout2(const GLB double* Us, const GLB double* dUs, double a0, double a1) {
+    STAMP0();
+    const int l = lanef();
+    const int grp = l >> 5, k = l & 31;
+    const double a_ = grp ? a1 : a0;
+    LDS double* ic = grp ? qs : inc;
+    LDS double* Xd = grp ? lam : Xt;
+    auto uk = [&](int j) { return Us[j] + a_ * dUs[j]; };
+    const double v = k < N ? uk(k * 6) : 0.0;
+    if (k < N) {
+#pragma unroll
+      for (int c = 0; c < 5; ++c) ic[k * 8 + c] = T * uk(k * 6 + 1 + c);
+    }
+    if (k < 8) ic[kZeroRow * 8 + k] = -0.0;
+    sync();
+    double a[5];
+    if (k <= N) {
+#pragma unroll
+      for (int c = 0; c < 5; ++c) a[c] = pp[3 + c];
+#pragma unroll
+      for (int j = 0; j < CAP::nmax; ++j) {
+        const LDS double* ij = ic + (j < k ? j : kZeroRow) * 8;
+#pragma unroll
+        for (int c = 0; c < 5; ++c) a[c] = a[c] + ij[c];
+      }
+      if (k < N) {
+        const double ct = cos(a[0]), st_ = sin(a[0]), cp = cos(a[1]), sp = sin(a[1]);
+        ic[k * 8 + 5] = T * (v * cp * ct);
+        ic[k * 8 + 6] = T * (v * sp * ct);
+        ic[k * 8 + 7] = T * (v * st_);
+      }
+    }
+    sync();
+    if (k <= N) {
+      double c0 = pp[0], c1 = pp[1], c2 = pp[2];
+#pragma unroll
+      for (int j = 0; j < CAP::nmax; ++j) {
+        const LDS double* ij = ic + (j < k ? j : kZeroRow) * 8;
+        c0 = c0 + ij[5];
+        c1 = c1 + ij[6];
+        c2 = c2 + ij[7];
+      }
+      LDS double* xk = Xd + k * 8;
+      xk[0] = c0; xk[1] = c1; xk[2] = c2;
+#pragma unroll
+      for (int c = 0; c < 5; ++c) xk[3 + c] = a[c];
+    }
+    STAMP1(PH_ROLLOUT);
+    sync();
+  }
+  // f and scaled rows of both trials (eval_fg's deep form): group 0 -> dt, f0; group 1 -> dms, f1
+  __device__ __forceinline__ void eval_fg2(double& f0, double& f1) {
+    STAMP0();
+    const int l = lanef();
+    const int grp = l >> 5, k = l & 31;
+    double f = 0.0;
+    if (k <= N) {
+      const LDS double* xk = (grp ? lam : Xt) + k * 8;
+      if (k < N) f = stage_cost(xk);
+      const double x0 = xk[0], x1 = xk[1];
+      double gv[CAP::mmax];
+#pragma unroll
+      for (int i = 0; i < CAP::mmax; ++i) {
+        const int oi = i - nb;
+        const int o = oi < 0 ? 0 : (oi < NMPC_MAX_OBS ? oi : NMPC_MAX_OBS - 1);
+        const double ddx = x0 - obx[o], ddy = x1 - oby[o];
+        const double ov = -sqrt(ddx * ddx + ddy * ddy) + P->orr[o];
+        gv[i] = i < 5 ? (i < nb ? xk[boxidx(i < 5 ? i : 0)] : ov) : ov;
+      }
+#pragma unroll
+      for (int i = 0; i < CAP::mmax; ++i) {
+        if (i < m) {
+          const int r = k * m + i;
+          const double v = dc[r] * gv[i];
+          if (grp) dms[r] = v;
+          else dt[r] = v;
+        }
+      }
+    }
+    sync();
+    f0 = wsum(grp ? 0.0 : f);
+    f1 = wsum(grp ? f : 0.0);
+    STAMP1(PH_EVAL);
+  }
+
   // --------------------------------------------- stage derivatives at X (lanef()=k)
   // gl[k] = grad l_k (8), Hl[k] = hess l_k packed over (x,y,z,x5,x6,x7), trig[k].
   // Derivation: oracle/nmpc_oracle.py::stage_cost_derivs (Q = (r1/a)^2+(r2/b)^2).
@@ -2184,9 +2281,13 @@ struct Solver {
     return pn_of(pn, lg, prox);
   }
   // restoration trial point: theta_R, phi_R and the original objective fo
+  // spec (kSpec classes): 0 this trial alone; 1 this trial and the next backtracking one
+  // (a2) formed together (rollout2 / eval_fg2; the second's objective into fo2); 2 this trial
+  // was formed as the second of a pair: its X in `lam`, its rows in `dms`, fo = fo2
   __device__ __forceinline__ bool trial_resto(double a, const GLB double* dUs, const RV* dss,
                                               const GLB double* dps, const GLB double* dns, double& fo,
-                                              double& phit, double& tht) {
+                                              double& phit, double& tht, int spec = 0, double a2 = 0.0,
+                                              double* fo2 = nullptr) {
     // the trial controls, their barrier terms and the proximity term in one pass (each
     // accumulator keeps the per-lane order of barrier_obj / resto_pn_terms)
     RSTAMP0(_trs);
@@ -2201,22 +2302,43 @@ struct Solver {
       if (on) prox += pv;
     });
     sync();
-    rollout(U, Xt, dUs, a);
-    fo = df * eval_fg(Xt, dt, dc);
-    // theta_R, the barrier sums and the p/n sums in one pass over the rows
     bool bad = false;
-    rows([&](int r, bool on) {
-      const double sv = s[r] + a * dss[r], pv = pR[r] + a * dps[r], nv = nR[r] + a * dns[r];
-      const double dtr = dt[r];
-      barrier_row(r, on, sv, logs, damp);
-      const double l2 = log(pv) + log(nv);
-      if (on) {
-        th += fabs(dtr - sv - pv + nv);
-        if (!isfinite(dtr)) bad = true;
-        pn += pv + nv;
-        lg += l2;
+    // theta_R, the barrier sums and the p/n sums in one pass over the rows
+    auto rowpass = [&](auto dtv) {
+      rows([&](int r, bool on) {
+        const double sv = s[r] + a * dss[r], pv = pR[r] + a * dps[r], nv = nR[r] + a * dns[r];
+        const double dtr = dtv[r];
+        barrier_row(r, on, sv, logs, damp);
+        const double l2 = log(pv) + log(nv);
+        if (on) {
+          th += fabs(dtr - sv - pv + nv);
+          if (!isfinite(dtr)) bad = true;
+          pn += pv + nv;
+          lg += l2;
+        }
+      });
+    };
+    bool done = false;
+    if constexpr (kSpec) {
+      if (spec == 2) {
+        fo = *fo2;
+        rowpass(dms);
+        done = true;
+      } else if (spec == 1) {
+        rollout2(U, dUs, a, a2);
+        double f0, f1;
+        eval_fg2(f0, f1);
+        fo = df * f0;
+        *fo2 = df * f1;
+        rowpass(dt);
+        done = true;
       }
-    });
+    }
+    if (!done) {
+      rollout(U, Xt, dUs, a);
+      fo = df * eval_fg(Xt, dt, dc);
+      rowpass(dt);
+    }
     tht = wsum(th);
     if (wany(bad)) return false;
     const double phb = barrier_fin(0.0, logs, damp);
@@ -2874,10 +2996,36 @@ __device__ __forceinline__ void resto_phase(const Params* __restrict__ prm, doub
         amin *= o.alpha_min_frac;
         a = rskip ? V[18] * o.alpha_red_factor : V[18];
         nsteps = 0;
+        // speculative pairs (Solver::kSpec): each trial not formed yet is formed together
+        // with the next backtracking trial (spec_a), whose X / rows wait in lam / dms
+        double spec_a = -1.0, spec_f = 0.0;
         while (a > amin || nsteps == 0) {
           double fo_t, ph, th;
-          const bool ok_t = S.trial_resto(a, S.dU, S.ds, S.dpR, S.dnR, fo_t, ph, th);
-          if (ok_t && r_check(a, ph, th)) { acc = 1; V[19] = a; V[20] = fo_t; V[21] = ph; a_test = a; break; }
+          bool ok_t;
+          const bool from_pair = Solver<CAP>::kSpec && a == spec_a;
+          if (from_pair) {
+            ok_t = S.trial_resto(a, S.dU, S.ds, S.dpR, S.dnR, fo_t, ph, th, 2, 0.0, &spec_f);
+            spec_a = -1.0;
+          } else {
+            const double an = a * o.alpha_red_factor;
+            ok_t = S.trial_resto(a, S.dU, S.ds, S.dpR, S.dnR, fo_t, ph, th, Solver<CAP>::kSpec ? 1 : 0, an, &spec_f);
+            spec_a = Solver<CAP>::kSpec ? an : -1.0;
+          }
+          if (ok_t && r_check(a, ph, th)) {
+            acc = 1; V[19] = a; V[20] = fo_t; V[21] = ph; a_test = a;
+            if (from_pair) {  // the accepted trial's X and rows into Xt / dt for the accept
+              if (S.lanef() <= N) {
+#pragma unroll
+                for (int c = 0; c < 8; ++c) S.Xt[S.lanef() * 8 + c] = S.lam[S.lanef() * 8 + c];
+              }
+              S.rows([&](int r, bool on) {
+                const double v = S.dms[r];
+                if (on) S.dt[r] = v;
+              });
+              sync();
+            }
+            break;
+          }
           if (ok_t && a == V[18] && V[15] <= th && o.max_soc > 0) {
             RSTAMP0(_soc);
             double th_tr = th, th_old = 0.0, a_soc = a;

@@ -24,3 +24,9 @@ for v in "$@"; do
   NMPC_LIB=$PWD/variants/$v.so timeout -k 10 200 python -u bench.py --no-per-step --no-cpu-baseline --batch 16384 > $O/${TAG}_${v}_wb.json 2> $O/${TAG}_${v}_wb.err || exit $?
 done
 echo ab done
+# the bounding chain alone (trace on), product and variants
+timeout -k 10 120 python -u scripts/chain_trace.py > $O/${TAG}_prod_chain.txt 2>&1 || exit $?
+for v in "$@"; do
+  NMPC_LIB=$PWD/variants/$v.so timeout -k 10 120 python -u scripts/chain_trace.py > $O/${TAG}_${v}_chain.txt 2>&1 || exit $?
+done
+echo chains done

@@ -89,3 +89,12 @@ chain = d.sum(0)
 print(f"and every step 15% faster (longest busy chain {chain.max():.1f} ms, work/slot {d.sum() / (NX * WPX):.1f} ms):")
 for name, f in policies.items():
     print(f"  {simulate(f):7.1f} ms  {name}")
+
+# what-if: max_iter steps (100 iterations, mostly restoration) f% faster, other steps unchanged
+z2 = np.load(sys.argv[1])
+d0 = (z2["times"][:, :, 1] - z2["times"][:, :, 0]).astype(np.float64) / 1e5
+for fct in (0.95, 0.9, 0.85, 0.8):
+    d = d0 * np.where(it >= 100, fct, 1.0)
+    chain = d.sum(0)
+    print(f"max_iter steps x{fct}: longest chain {chain.max():.1f} ms, current policy "
+          f"{simulate(policies['current: hot (prev >= 50 its) first, lowest step, FIFO']):.1f} ms")
