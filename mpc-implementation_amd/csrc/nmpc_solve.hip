@@ -389,17 +389,27 @@ struct Solver {
   // `for (r = lane; r < ng; r += 64)` with loads under `if (hasl(..))` waits on
   // memory several times per trip).  Per lane the rows are still visited in
   // increasing order, so reductions are bitwise those of the plain loop.
-  template <class F>
+  template <int RU = CAP::ru, class F>
   __device__ __forceinline__ void rows(F&& f) const {
-    for (int base = 0; base < ng; base += CAP::ru * WAVE) {
+    for (int base = 0; base < ng; base += RU * WAVE) {
 #pragma unroll
-      for (int u = 0; u < CAP::ru; ++u) {
+      for (int u = 0; u < RU; ++u) {
         const int r = base + u * WAVE + lanef();
         const bool on = r < ng;
         f(on ? r : ng - 1, on);
       }
     }
   }
+  // the restoration phase's row passes read its global row vectors (p, n, their
+  // multipliers and steps) besides the LDS rows: in the LDS-row class they take more trips
+  // per group (fewer global round trips per pass); per lane the rows are still visited in
+  // increasing order, so the sums are bitwise those of rows()
+#ifndef NMPC_RESTO_RU
+#define NMPC_RESTO_RU 2
+#endif
+  static constexpr int kRestoRU = CAP::lds_rows ? (NMPC_RESTO_RU < CAP::rtrips ? NMPC_RESTO_RU : CAP::rtrips) : CAP::ru;
+  template <class F>
+  __device__ __forceinline__ void rows_r(F&& f) const { rows<kRestoRU>(static_cast<F&&>(f)); }
   // the same for the decision variables (index clamped to the last one when off: every
   // load is valid, so a pass's loads over its trips issue together; f guards its sums and
   // stores with `on`)
@@ -1466,14 +1476,32 @@ struct Solver {
       const LDS double* xk = X + k * 8;
       double Qxy0 = 0, Qxy1 = 0, Qxy2 = 0, qx = 0, qy = 0;
       double Qb[5] = {0, 0, 0, 0, 0}, qb[5] = {0, 0, 0, 0, 0};
+      // global-row classes: the next row's four operands are fetched while this row is
+      // folded (one row ahead: a global load's latency per row instead of per operand set;
+      // blocks of five rows spilled in the register-limited classes); the LDS
+      // class reads them at use
+      double nW = 0.0, nB = 0.0, nY = 0.0, nD = 0.0;
+      if constexpr (!CAP::lds_rows) {
+        const int r0 = k * m;
+        nW = soc ? 0.0 : Wr[r0]; nB = Br[r0]; nY = y[r0]; nD = dc[r0];
+      }
       for (int i = 0; i < m; ++i) {
         const int r = k * m + i;
-        const double w = soc ? 0.0 : Wr[r], bw = Br[r];
+        double w, bw, yr, dcr;
+        if constexpr (!CAP::lds_rows) {
+          w = nW; bw = nB; yr = nY; dcr = nD;
+          const int rn = i + 1 < m ? r + 1 : r;
+          nW = soc ? 0.0 : Wr[rn]; nB = Br[rn]; nY = y[rn]; nD = dc[rn];
+        } else {
+          w = soc ? 0.0 : Wr[r]; bw = Br[r];
+        }
         if (i < nb) {
           Qb[i] = w;
           qb[i] = bw;
         } else {
-          const double C = curv ? y[r] * dc[r] : 0.0;
+          double C;
+          if constexpr (!CAP::lds_rows) C = curv ? yr * dcr : 0.0;
+          else C = curv ? y[r] * dc[r] : 0.0;
           const int o = i - nb;
           const double ddx = xk[0] - obx[o], ddy = xk[1] - oby[o];
           const double idd = rsq(ddx * ddx + ddy * ddy);
@@ -2199,7 +2227,7 @@ struct Solver {
                                                  double tau_, double& ap, double& ad) {
     const double kd = P->o.kappa_d;
     th = 0.0; gsum = 0.0; ap = 1.0; ad = 1.0;
-    rows([&](int r, bool on) {
+    rows_r([&](int r, bool on) {
       const int k = r / m, i = r - k * m;
       const LDS double* xk = X + k * 8;
       const LDS double* dxk = dXs + k * 8;
@@ -2264,7 +2292,7 @@ struct Solver {
   __device__ __forceinline__ double resto_pn_terms(const GLB double* Us, double a, const GLB double* dps,
                                                    const GLB double* dns) {
     double pn = 0.0, lg = 0.0, prox = 0.0;
-    rows([&](int r, bool on) {
+    rows_r([&](int r, bool on) {
       const double pv = dps ? pR[r] + a * dps[r] : pR[r], nv = dns ? nR[r] + a * dns[r] : nR[r];
       const double l2 = log(pv) + log(nv);
       if (on) {
@@ -2305,7 +2333,7 @@ struct Solver {
     bool bad = false;
     // theta_R, the barrier sums and the p/n sums in one pass over the rows
     auto rowpass = [&](auto dtv) {
-      rows([&](int r, bool on) {
+      rows_r([&](int r, bool on) {
         const double sv = s[r] + a * dss[r], pv = pR[r] + a * dps[r], nv = nR[r] + a * dns[r];
         const double dtr = dtv[r];
         barrier_row(r, on, sv, logs, damp);
@@ -2723,7 +2751,7 @@ __device__ __forceinline__ void resto_phase(const Params* __restrict__ prm, doub
           const double sz = fabs(S.zl[i]) + fabs(S.zu[i]), fx = S.dr2(i) * dd * dd;
           if (on) { sumz += sz; frx += fx; }
         });
-        S.rows([&](int r, bool on) {
+        S.rows_r([&](int r, bool on) {
           const double yr = S.y[r], pr = S.pR[r], nr = S.nR[r], vlr = S.vl[r], vur = S.vu[r];
           const double zp = S.zpR[r], zn = S.znR[r], dr = S.d[r], sr = S.s[r], dcr = S.dc[r];
           const double lo = S.dl[r], hi = S.du[r];
@@ -2793,7 +2821,7 @@ __device__ __forceinline__ void resto_phase(const Params* __restrict__ prm, doub
               if (S.hasl(S.xl[i])) cm = fmax(cm, fabs((S.U[i] - S.xl[i]) * S.zl[i] - mu_));
               if (S.hasu(S.xu[i])) cm = fmax(cm, fabs((S.xu[i] - S.U[i]) * S.zu[i] - mu_));
             });
-            S.rows([&](int r, bool on) {
+            S.rows_r([&](int r, bool on) {
               const double yr = S.y[r], vlr = S.vl[r], vur = S.vu[r], zp = S.zpR[r], zn = S.znR[r];
               const double sr = S.s[r], dr = S.d[r], pr = S.pR[r], nr = S.nR[r], lo = S.dl[r], hi = S.du[r];
               const double dv = fmax(S.eqlo(lo) ? 0.0 : fabs(-yr - vlr + vur), fmax(fabs(rho - yr - zp), fabs(rho + yr - zn)));
@@ -3093,6 +3121,8 @@ __device__ __forceinline__ void resto_phase(const Params* __restrict__ prm, doub
           const double ad = (acc == 1 && rftb_ok && !rwd_dir) ? rftb_d
                                                                : S.dual_frac_to_bound_resto(V[5], dUa, dsa, dpa, dna);
           const double muA = V[4];  // volatile LDS scalar read once
+          // (the accepted controls U <- Ut in the same pass: each lane reads its U[i] for the
+          // dual step before it writes it)
           S.ctrls([&](int i, bool on) {
             double dzl, dzu;
             S.dz_x(i, dUa[i], dzl, dzu);
@@ -3102,12 +3132,12 @@ __device__ __forceinline__ void resto_phase(const Params* __restrict__ prm, doub
             else nzl = 0.0;
             if (S.hasu(S.xu[i])) { const double Sn = S.xu[i] - un; nzu = fmax(fmin(nzu, ks * muA / Sn), muA / (ks * Sn)); }
             else nzu = 0.0;
-            if (on) { S.zl[i] = nzl; S.zu[i] = nzu; }
+            if (on) { S.zl[i] = nzl; S.zu[i] = nzu; S.U[i] = un; }
           });
           const double muR = V[4], aP = V[19];  // volatile LDS scalars read once
           const double dmuR = rwd_dir ? (double)WD[4] : muR;
           double tho = 0.0;  // theta of the original problem at the new iterate (next check)
-          S.rows([&](int r, bool on) {
+          S.rows_r([&](int r, bool on) {
             const double sr = S.s[r], lo = S.dl[r], hi = S.du[r], vlr = S.vl[r], vur = S.vu[r];
             const double dsr = dsa[r], dpr = dpa[r], dnr = dna[r], dyr = dya[r];
             const double pr = S.pR[r], nr = S.nR[r], zp = S.zpR[r], zn = S.znR[r], yr = S.y[r], dtr = S.dt[r];
@@ -3140,10 +3170,6 @@ __device__ __forceinline__ void resto_phase(const Params* __restrict__ prm, doub
           tho = wsum(tho);
           V[22] = tho;
           S.mu = V[4];
-          S.ctrls([&](int i, bool on) {
-            const double ut = S.Ut[i];
-            if (on) S.U[i] = ut;
-          });
           if (S.lanef() <= N) {
 #pragma unroll
             for (int c = 0; c < 8; ++c) S.X[S.lanef() * 8 + c] = S.Xt[S.lanef() * 8 + c];
@@ -4058,6 +4084,8 @@ __device__ __forceinline__ int solve_one(Solver<CAP>& S, const Params* __restric
       const double ap = alpha_p, ad = alpha_d;
       const double ks = o.kappa_sigma;
       // bound multipliers of U (old slacks for the step, new slacks for kappa_sigma)
+      // (the accepted controls U <- Ut in the same pass: each lane reads its U[i] for the
+      // dual step before it writes it)
       S.ctrls([&](int i, bool on) {
         double dzl, dzu;
         S.dz_x(i, dUa[i], dzl, dzu);
@@ -4067,7 +4095,7 @@ __device__ __forceinline__ int solve_one(Solver<CAP>& S, const Params* __restric
         else nzl = 0.0;
         if (S.hasu(S.xu[i])) { const double Sn = S.xu[i] - un; nzu = fmax(fmin(nzu, ks * mu / Sn), mu / (ks * Sn)); }
         else nzu = 0.0;
-        if (on) { S.zl[i] = nzl; S.zu[i] = nzu; }
+        if (on) { S.zl[i] = nzl; S.zu[i] = nzu; S.U[i] = un; }
       });
       const double kdm = o.kappa_d * S.mu, dlt = S.delta;
       S.rows([&](int r, bool on) {
@@ -4095,10 +4123,6 @@ __device__ __forceinline__ int solve_one(Solver<CAP>& S, const Params* __restric
         }
       });
       S.mu = mu;
-      S.ctrls([&](int i, bool on) {
-        const double ut = S.Ut[i];
-        if (on) S.U[i] = ut;
-      });
       if (S.lanef() <= N) {
 #pragma unroll
         for (int c = 0; c < 8; ++c) S.X[S.lanef() * 8 + c] = S.Xt[S.lanef() * 8 + c];

@@ -263,3 +263,26 @@ def reference_bounds_literal(N, m_rows=8, n_obs=3, stop=128):
                                   (-math.pi / 30, math.pi / 30)]):
         lbx[j:6 * N:6] = lo; ubx[j:6 * N:6] = hi
     return lbx, ubx, lbg, ubg
+
+
+def test_oracle_records_restoration_checks():
+    """The oracle's convergence-check record (the parity tests' termination margins) holds
+    the restoration NLP's own checks too (resto=True), as the kernel's trace does (negative
+    error in fields 8..11): an Infeasible_Problem_Detected step of the 10_obstacles.py run
+    ends on such a check, converged (scaled NLP error at or below tol)."""
+    import os
+    import sys
+    GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+    sys.path.insert(0, GOLD)
+    from gen_reference_runs import run_problem, warm_start
+    z = np.load(os.path.join(GOLD, "ref_run_10_obstacles.npz"))
+    prob = run_problem("10_obstacles")
+    ipo = orc.IpoptDense(prob, orc.REFERENCE_OPTS)
+    tol = orc.REFERENCE_OPTS.get("tol", orc.IPOPT_DEFAULTS["tol"])
+    k = int(np.flatnonzero(z["status"] == orc.INFEASIBLE_PROBLEM_DETECTED)[0])
+    w = warm_start(z["x"][k - 1]) if k > 0 else np.zeros(prob.nw)
+    r = ipo.solve(w, z["lbx"], z["ubx"], z["lbg"], z["ubg"], z["p"][k], trace=True)
+    res = [c for c in ipo.chk if c.get("resto")]
+    assert r["status"] == orc.INFEASIBLE_PROBLEM_DETECTED and r["iter"] == z["iter"][k]
+    assert res and res[-1]["it"] == r["iter"] and res[-1]["err"] <= tol
+    assert all(c["err"] > tol for c in res[:-1] if c["it"] < r["iter"] - 1) or len(res) == 1
