@@ -1431,7 +1431,11 @@ struct Solver {
     auto Wr = ds2;
     auto Br = dt;
     const bool curv = !(mode == SUM_LS || mode == SUM_LS_RESTO);  // y-weighted row curvature
-    rows([&](int r, bool on) {
+    auto rowsA = [&](auto&& body) {  // the restoration modes read its global row vectors: rows_r
+      if (mode == SUM_RESTO || mode == SUM_RESTO_SOC || mode == SUM_LS_RESTO) rows_r(body);
+      else rows(body);
+    };
+    rowsA([&](int r, bool on) {
       const double dcr = dc[r];
       double A, Bw;
       if (mode == SUM_LS) {
@@ -1476,32 +1480,14 @@ struct Solver {
       const LDS double* xk = X + k * 8;
       double Qxy0 = 0, Qxy1 = 0, Qxy2 = 0, qx = 0, qy = 0;
       double Qb[5] = {0, 0, 0, 0, 0}, qb[5] = {0, 0, 0, 0, 0};
-      // global-row classes: the next row's four operands are fetched while this row is
-      // folded (one row ahead: a global load's latency per row instead of per operand set;
-      // blocks of five rows spilled in the register-limited classes); the LDS
-      // class reads them at use
-      double nW = 0.0, nB = 0.0, nY = 0.0, nD = 0.0;
-      if constexpr (!CAP::lds_rows) {
-        const int r0 = k * m;
-        nW = soc ? 0.0 : Wr[r0]; nB = Br[r0]; nY = y[r0]; nD = dc[r0];
-      }
       for (int i = 0; i < m; ++i) {
         const int r = k * m + i;
-        double w, bw, yr, dcr;
-        if constexpr (!CAP::lds_rows) {
-          w = nW; bw = nB; yr = nY; dcr = nD;
-          const int rn = i + 1 < m ? r + 1 : r;
-          nW = soc ? 0.0 : Wr[rn]; nB = Br[rn]; nY = y[rn]; nD = dc[rn];
-        } else {
-          w = soc ? 0.0 : Wr[r]; bw = Br[r];
-        }
+        const double w = soc ? 0.0 : Wr[r], bw = Br[r];
         if (i < nb) {
           Qb[i] = w;
           qb[i] = bw;
         } else {
-          double C;
-          if constexpr (!CAP::lds_rows) C = curv ? yr * dcr : 0.0;
-          else C = curv ? y[r] * dc[r] : 0.0;
+          const double C = curv ? y[r] * dc[r] : 0.0;
           const int o = i - nb;
           const double ddx = xk[0] - obx[o], ddy = xk[1] - oby[o];
           const double idd = rsq(ddx * ddx + ddy * ddy);
@@ -1598,7 +1584,7 @@ struct Solver {
     LDS R* pn = (LDS R*)pvb;
     LDS R* Stc = (LDS R*)St;
     LDS R* Rcc = (LDS R*)Rc;
-    LDS R* rvs = (LDS R*)Rv;  // r_k of the current stage (lanes 0..5 publish, every lane reads)
+    LDS R* rts = (LDS R*)Rv;  // r~ = r_k + B_k^T p_{k+1} of the current stage (lanes 0..5 form it)
     // wave-uniform scalars of the loop held in VGPRs: as SGPR pairs they are spilled to
     // VGPR lanes and restored (v_readlane pair + s_nop) at every use inside the sweep
     double Tv = T;
@@ -1640,6 +1626,25 @@ struct Solver {
     //   S~ row 0 adds s03 (j = 3) / s04 (j = 4)
     const R ms3 = (i == 0 && j == 3) ? (R)1 : (R)0, ms4 = (i == 0 && j == 4) ? (R)1 : (R)0;
     const bool absent = diagR && rR >= nuE;  // absent control (model embedding): unit pivot
+    // Per-lane store targets fixed for the sweep (no address arithmetic, no divergent
+    // branch around the stores inside it): lanes without an S~ / R~ / r~ entry store to
+    // slots of the trial rows `dt`, which are dead during a factorisation (rewritten by the
+    // next trial before any read), in the classes that keep dt in LDS; K column ln (lanes
+    // 0..7) and R~ entry tR are stored through per-lane base pointers
+    constexpr bool kDummy = CAP::lds_rows && !CAP::refine;
+    LDS R* dmy = kDummy ? (LDS R*)dt : Stc;
+    LDS R* const st_dst = ln < 48 ? Stc + ln : dmy + ln;
+    LDS R* const rc_dst = tR0 >= 0 ? Rcc + tR : dmy + 64 + ln;
+    LDS R* const rt_dst = ln < 6 ? rts + ln : dmy + 128 + ln;
+    GLB double* const Kl = K + (ln < 8 ? ln : 0);
+    GLB double* const Rkl = Rk + tR;
+    // lane 8 carries r~ through the triangular solves: its right-hand-side column is rts
+    LDS R* const bcol = ln == 8 ? rts : Stc + j;
+    const int bstr = ln == 8 ? 1 : 8;
+    // per-lane bases of the prefetched stage operands
+    const GLB double* const Qsl = Qs + ij;
+    const GLB double* const Rdl = Rd + rR;
+    const GLB double* const rvl = rv + lr;
     sync();
     bool ok = true;
     // one stage of the backward sweep (false: a pivot is not positive)
@@ -1696,10 +1701,29 @@ struct Solver {
           if ((fm >> i) & 1) stv = zr;
           if (((fm >> rR) | (fm >> cR)) & 1) v = (rR == cR) ? (R)1 : zr;
         }
-        if (ln < 48) Stc[ln] = stv;
-        if (tR0 >= 0) Rcc[tR] = v;
-        Rk[k * 21 + tR] = (double)v;
-        if (ln < 6) rvs[ln] = rvk;
+        // r~ entry lr = r_k[lr] + (B_k^T p_{k+1})[lr] (lanes 0..5; both forms, selected).
+        // The contractions are spelled out: selecting between the two forms lets the
+        // compiler hoist the add of r_k out of the select and leave Tr * p unfused, a
+        // different rounding from the single fused form every other solve of r~ uses
+        R rtv;
+        {
+          const R rt0 = rvk + fma(b20, pc[2], fma(b00, pc[0], b10 * pc[1]));
+          const R rtc = fma(Tr, pc[2 + lr], rvk);
+          rtv = lr == 0 ? rt0 : rtc;
+          if (fm != 0) {
+            if ((fm >> lr) & 1) rtv = zr;
+          }
+        }
+        if constexpr (kDummy) {
+          *st_dst = stv;
+          *rc_dst = v;
+          *rt_dst = rtv;
+        } else {
+          if (ln < 48) *st_dst = stv;
+          if (tR0 >= 0) *rc_dst = v;
+          if (ln < 6) *rt_dst = rtv;
+        }
+        Rkl[k * 21] = (double)v;
         sync();
         STAMP1(PH_RA); }
       // ---- (2)
@@ -1740,20 +1764,14 @@ struct Solver {
             }
           }
         }
-        rt[0] = rvs[0] + ((b00 * pc[0] + b10 * pc[1]) + b20 * pc[2]);
 #pragma unroll
-        for (int r = 1; r < 6; ++r) rt[r] = rvs[r] + Tr * pc[2 + r];
-        if (fm != 0) {
-#pragma unroll
-          for (int r = 0; r < 6; ++r)
-            if ((fm >> r) & 1) rt[r] = zr;
-        }
+        for (int r = 0; r < 6; ++r) rt[r] = rts[r];
         R ya[6], yb[6];
 #pragma unroll
         for (int r = 0; r < 6; ++r) {
           R a = Stc[r * 8 + i];
-          R bb = Stc[r * 8 + j];
-          if (ln == 8) bb = rt[r];
+          R bb = bcol[r * bstr];
+
 #pragma unroll
           for (int t = 0; t < r; ++t) {
             a -= Lm[r * (r + 1) / 2 + t] * ya[t];
@@ -1779,29 +1797,33 @@ struct Solver {
           for (int r = 0; r < 6; ++r) yb[r] *= sg[r];
         }
         // back substitution: lanes 0..7 column ln of K, lane 8 k = -R~^-1 r~ (every lane
-        // computes it: branch-free, so it overlaps with the next stage's LDS reads)
+        // computes it: branch-free, so it overlaps with the next stage's LDS reads), carried
+        // negated (mb = -yb: negation commutes with every rounding, so the same values), so
+        // K and k_k are stored without a negation
+        R mb[6];
 #pragma unroll
         for (int r = 5; r >= 0; --r) {
-          R a = yb[r];
+          R a = -yb[r];
 #pragma unroll
-          for (int t = r + 1; t < 6; ++t) a -= Lm[t * (t + 1) / 2 + r] * yb[t];
-          yb[r] = a * idg[r];
+          for (int t = r + 1; t < 6; ++t) a -= Lm[t * (t + 1) / 2 + r] * mb[t];
+          mb[r] = a * idg[r];
         }
         R atp = pc[j];
         atp = atp + mj3 * ((E03 * pc[0] + E13 * pc[1]) + E23 * pc[2]) + mj4 * (E04 * pc[0] + E14 * pc[1]);
         R kr = zr;
 #pragma unroll
-        for (int r = 0; r < 6; ++r) kr += (-yb[r]) * rt[r];
+        for (int r = 0; r < 6; ++r) kr += mb[r] * rt[r];
         const R pnv = ((R)qs[k * 10 + j] + atp) + kr;
         if (ln < 8) {
+          GLB double* Kk = Kl + k * 48;
 #pragma unroll
-          for (int r = 0; r < 6; ++r) K[k * 48 + r * 8 + ln] = (double)(-yb[r]);
+          for (int r = 0; r < 6; ++r) Kk[r * 8] = (double)mb[r];
         }
         if (ln < 8) {
           pn[ln] = pnv;
         } else if (ln == 8) {
 #pragma unroll
-          for (int r = 0; r < 6; ++r) kf[k * 6 + r] = (double)(-yb[r]);
+          for (int r = 0; r < 6; ++r) kf[k * 6 + r] = (double)mb[r];
         }
         sync();
         STAMP1(PH_RD); }
@@ -1817,12 +1839,12 @@ struct Solver {
     for (int k = N - 1; k >= 0; k -= 2) {
       {
         const int kp = k > 0 ? k - 1 : 0;
-        qB = Qs[kp * 36 + ij]; rB = Rd[kp * 6 + rR]; vB = rv[kp * 6 + lr];
+        qB = Qsl[kp * 36]; rB = Rdl[kp * 6]; vB = rvl[kp * 6];
       }
       if (!stage(k, qvn, rdn, rvn) || k == 0) break;
       {
         const int kp = k > 1 ? k - 2 : 0;
-        qvn = Qs[kp * 36 + ij]; rdn = Rd[kp * 6 + rR]; rvn = rv[kp * 6 + lr];
+        qvn = Qsl[kp * 36]; rdn = Rdl[kp * 6]; rvn = rvl[kp * 6];
       }
       if (!stage(k - 1, qB, rB, vB)) break;
     }
