@@ -1853,7 +1853,12 @@ struct Solver {
   }
 
   // gradient-only re-solve with the stored factors (second-order correction):
-  // every lanef() runs the vector recursion redundantly (R~_k re-factorised).
+  // every lanef() runs the vector recursion p_k = q_k + A_k^T p_{k+1} + K_k^T r~_k
+  // redundantly; it needs r~_k = r_k + B_k^T p_{k+1} but not k_k = -R~_k^-1 r~_k, so the
+  // stages' re-factorisations of R~_k and their solves for k_k leave the serial sweep: lane
+  // k keeps its stage's r~_k and, after the sweep, factorises its own R~_k and solves for
+  // k_k, all stages at once (the same operations in the same order as in the sweep: the
+  // same values)
   // ZQ: linear state terms q_k = 0 (the refinement's right-hand side is a control residual)
   template <bool ZQ = false>
   __device__ __forceinline__ void resolve(const GLB double* rv) {
@@ -1862,18 +1867,75 @@ struct Solver {
 #endif
     STAMP0();
     using R = typename CAP::RT;  // the factorisation's precision
+    const int ln = lanef();
     R p8[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) p8[i] = ZQ ? (R)0 : (R)qs[N * 10 + i];
-    // one stage of the backward recursion with its stored R~_k (Lin) and r_k (rin)
-    auto stage = [&](int k, const R (&Lin)[21], const R (&rin)[6]) {
+    R rtk[6];  // r~ of stage ln (CAP::nmax < WAVE: one stage per lane)
+#pragma unroll
+    for (int r = 0; r < 6; ++r) rtk[r] = (R)0;
+    // one stage of the backward recursion with its stored r_k (rin)
+    auto stage = [&](int k, const R (&rin)[6]) {
       double E03d, E04d, E13d, E14d, E23d, b00d, b10d, b20d;
       stage_AB(k, E03d, E04d, E13d, E14d, E23d, b00d, b10d, b20d);
       const R E03 = (R)E03d, E04 = (R)E04d, E13 = (R)E13d, E14 = (R)E14d, E23 = (R)E23d;
       const R b00 = (R)b00d, b10 = (R)b10d, b20 = (R)b20d, Tr = (R)T;
-      R Lm[21], idg[6], rt[6], v[6];
+      R rt[6];
+      rt[0] = rin[0] + ((b00 * p8[0] + b10 * p8[1]) + b20 * p8[2]);
 #pragma unroll
-      for (int t = 0; t < 21; ++t) Lm[t] = Lin[t];
+      for (int r = 1; r < 6; ++r) rt[r] = rin[r] + Tr * p8[2 + r];
+      if (nfix > 0) {
+        const int fm = fixm[k];
+#pragma unroll
+        for (int r = 0; r < 6; ++r)
+          if ((fm >> r) & 1) rt[r] = (R)0;
+      }
+      const bool mine = ln == k;
+#pragma unroll
+      for (int r = 0; r < 6; ++r) rtk[r] = mine ? rt[r] : rtk[r];
+      R pn[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        R atp = p8[i];
+        if (i == 3) atp = atp + ((E03 * p8[0] + E13 * p8[1]) + E23 * p8[2]);
+        else if (i == 4) atp = atp + (E04 * p8[0] + E14 * p8[1]);
+        R kr = (R)0;
+#pragma unroll
+        for (int r = 0; r < 6; ++r) kr += (R)K[k * 48 + r * 8 + i] * rt[r];
+        pn[i] = ((ZQ ? (R)0 : (R)qs[k * 10 + i]) + atp) + kr;
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i) p8[i] = pn[i];
+    };
+    // the stored r_k do not depend on the recursion: stage k-1's are fetched while stage k
+    // is formed (two stages per trip, alternating register sets; clamped fetches)
+    R rA[6], rB[6];
+    auto fetch = [&](R (&ro)[6], int ks) {
+      const int kc = ks > 0 ? ks : 0;
+#pragma unroll
+      for (int r = 0; r < 6; ++r) ro[r] = (R)rv[kc * 6 + r];
+    };
+    if constexpr (CAP::deep) {
+      fetch(rA, N - 1);
+      for (int k = N - 1; k >= 0; k -= 2) {
+        fetch(rB, k - 1);
+        stage(k, rA);
+        if (k == 0) break;
+        fetch(rA, k - 2);
+        stage(k - 1, rB);
+      }
+    } else {
+      (void)rB;
+      for (int k = N - 1; k >= 0; --k) {
+        fetch(rA, k);
+        stage(k, rA);
+      }
+    }
+    // k_k = -R~_k^-1 r~_k, lane k: R~_k's Cholesky factor and the two triangular solves
+    if (ln < N) {
+      R Lm[21], idg[6], v[6];
+#pragma unroll
+      for (int t = 0; t < 21; ++t) Lm[t] = (R)Rk[ln * 21 + t];
 #pragma unroll
       for (int c = 0; c < 6; ++c) {
         R dg = Lm[c * (c + 1) / 2 + c];
@@ -1890,18 +1952,9 @@ struct Solver {
           Lm[r * (r + 1) / 2 + c] = a * ig;
         }
       }
-      rt[0] = rin[0] + ((b00 * p8[0] + b10 * p8[1]) + b20 * p8[2]);
-#pragma unroll
-      for (int r = 1; r < 6; ++r) rt[r] = rin[r] + Tr * p8[2 + r];
-      if (nfix > 0) {
-        const int fm = fixm[k];
-#pragma unroll
-        for (int r = 0; r < 6; ++r)
-          if ((fm >> r) & 1) rt[r] = (R)0;
-      }
 #pragma unroll
       for (int r = 0; r < 6; ++r) {
-        R a = rt[r];
+        R a = rtk[r];
 #pragma unroll
         for (int t = 0; t < r; ++t) a -= Lm[r * (r + 1) / 2 + t] * v[t];
         v[r] = a * idg[r];
@@ -1913,49 +1966,8 @@ struct Solver {
         for (int t = r + 1; t < 6; ++t) a -= Lm[t * (t + 1) / 2 + r] * v[t];
         v[r] = a * idg[r];
       }
-      if (lanef() == 0) {
 #pragma unroll
-        for (int r = 0; r < 6; ++r) kf[k * 6 + r] = (double)(-v[r]);
-      }
-      R pn[8];
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        R atp = p8[i];
-        if (i == 3) atp = atp + ((E03 * p8[0] + E13 * p8[1]) + E23 * p8[2]);
-        else if (i == 4) atp = atp + (E04 * p8[0] + E14 * p8[1]);
-        R kr = (R)0;
-#pragma unroll
-        for (int r = 0; r < 6; ++r) kr += (R)K[k * 48 + r * 8 + i] * rt[r];
-        pn[i] = ((ZQ ? (R)0 : (R)qs[k * 10 + i]) + atp) + kr;
-      }
-#pragma unroll
-      for (int i = 0; i < 8; ++i) p8[i] = pn[i];
-    };
-    // the stored R~_k and r_k do not depend on the recursion: stage k-1's are fetched while
-    // stage k is formed (two stages per trip, alternating register sets; clamped fetches)
-    R LA[21], LB[21], rA[6], rB[6];
-    auto fetch = [&](R (&Lo)[21], R (&ro)[6], int ks) {
-      const int kc = ks > 0 ? ks : 0;
-#pragma unroll
-      for (int t = 0; t < 21; ++t) Lo[t] = (R)Rk[kc * 21 + t];
-#pragma unroll
-      for (int r = 0; r < 6; ++r) ro[r] = (R)rv[kc * 6 + r];
-    };
-    if constexpr (CAP::deep) {
-      fetch(LA, rA, N - 1);
-      for (int k = N - 1; k >= 0; k -= 2) {
-        fetch(LB, rB, k - 1);
-        stage(k, LA, rA);
-        if (k == 0) break;
-        fetch(LA, rA, k - 2);
-        stage(k - 1, LB, rB);
-      }
-    } else {
-      (void)LB; (void)rB;
-      for (int k = N - 1; k >= 0; --k) {
-        fetch(LA, rA, k);
-        stage(k, LA, rA);
-      }
+      for (int r = 0; r < 6; ++r) kf[ln * 6 + r] = (double)(-v[r]);
     }
     sync();
     STAMP1(PH_RESOLVE);
