@@ -1852,13 +1852,16 @@ struct Solver {
     return ok;
   }
 
-  // gradient-only re-solve with the stored factors (second-order correction):
-  // every lanef() runs the vector recursion p_k = q_k + A_k^T p_{k+1} + K_k^T r~_k
-  // redundantly; it needs r~_k = r_k + B_k^T p_{k+1} but not k_k = -R~_k^-1 r~_k, so the
-  // stages' re-factorisations of R~_k and their solves for k_k leave the serial sweep: lane
-  // k keeps its stage's r~_k and, after the sweep, factorises its own R~_k and solves for
-  // k_k, all stages at once (the same operations in the same order as in the sweep: the
-  // same values)
+  // gradient-only re-solve with the stored factors (second-order correction): the vector
+  // recursion p_k = q_k + A_k^T p_{k+1} + K_k^T r~_k, r~_k = r_k + B_k^T p_{k+1}.
+  //  - Lane i < 8 forms p_k[i] (row i: its K_k column, prefetched a stage ahead) and
+  //    publishes it through LDS; every lane reads p_{k+1} back and forms r~_k.
+  //  - k_k = -R~_k^-1 r~_k is not needed by the recursion, so the stages' re-factorisations
+  //    of R~_k and their solves leave the serial sweep: lane k keeps its stage's r~_k and,
+  //    after the sweep, factorises its own R~_k and solves for k_k, all stages at once.
+  // Every value is formed by the same operations in the same order as when every lane ran
+  // the whole recursion (row i's expressions are written out per kind, as before): the
+  // same bits.
   // ZQ: linear state terms q_k = 0 (the refinement's right-hand side is a control residual)
   template <bool ZQ = false>
   __device__ __forceinline__ void resolve(const GLB double* rv) {
@@ -1868,18 +1871,25 @@ struct Solver {
     STAMP0();
     using R = typename CAP::RT;  // the factorisation's precision
     const int ln = lanef();
-    R p8[8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) p8[i] = ZQ ? (R)0 : (R)qs[N * 10 + i];
+    const int li = ln < 8 ? ln : 7;  // the row of p this lane forms (lanes >= 8 duplicate row 7)
+    LDS R* pv = (LDS R*)pva;         // p_{k+1}, published by lanes 0..7
+    if (ln < 8) pv[ln] = ZQ ? (R)0 : (R)qs[N * 10 + ln];
     R rtk[6];  // r~ of stage ln (CAP::nmax < WAVE: one stage per lane)
 #pragma unroll
     for (int r = 0; r < 6; ++r) rtk[r] = (R)0;
-    // one stage of the backward recursion with its stored r_k (rin)
-    auto stage = [&](int k, const R (&rin)[6]) {
+    const GLB double* const Kl = K + li;  // this lane's K column: K_k[r][li] = Kl[k*48 + r*8]
+    sync();
+    // one stage of the backward recursion with its stored r_k (rin) and K column (kc)
+    auto stage = [&](int k, const R (&rin)[6], const R (&kc)[6]) {
       double E03d, E04d, E13d, E14d, E23d, b00d, b10d, b20d;
       stage_AB(k, E03d, E04d, E13d, E14d, E23d, b00d, b10d, b20d);
       const R E03 = (R)E03d, E04 = (R)E04d, E13 = (R)E13d, E14 = (R)E14d, E23 = (R)E23d;
       const R b00 = (R)b00d, b10 = (R)b10d, b20 = (R)b20d, Tr = (R)T;
+      R p8[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) p8[i] = pv[i];
+      const R pl = pv[li];
+      const R ql = ZQ ? (R)0 : (R)qs[k * 10 + li];
       R rt[6];
       rt[0] = rin[0] + ((b00 * p8[0] + b10 * p8[1]) + b20 * p8[2]);
 #pragma unroll
@@ -1893,43 +1903,36 @@ struct Solver {
       const bool mine = ln == k;
 #pragma unroll
       for (int r = 0; r < 6; ++r) rtk[r] = mine ? rt[r] : rtk[r];
-      R pn[8];
+      // (A^T p)[li]: rows 3 and 4 add the E column terms (both formed, selected by row)
+      const R at3 = pl + ((E03 * p8[0] + E13 * p8[1]) + E23 * p8[2]);
+      const R at4 = pl + (E04 * p8[0] + E14 * p8[1]);
+      const R atp = li == 3 ? at3 : (li == 4 ? at4 : pl);
+      R kr = (R)0;
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        R atp = p8[i];
-        if (i == 3) atp = atp + ((E03 * p8[0] + E13 * p8[1]) + E23 * p8[2]);
-        else if (i == 4) atp = atp + (E04 * p8[0] + E14 * p8[1]);
-        R kr = (R)0;
-#pragma unroll
-        for (int r = 0; r < 6; ++r) kr += (R)K[k * 48 + r * 8 + i] * rt[r];
-        pn[i] = ((ZQ ? (R)0 : (R)qs[k * 10 + i]) + atp) + kr;
-      }
-#pragma unroll
-      for (int i = 0; i < 8; ++i) p8[i] = pn[i];
+      for (int r = 0; r < 6; ++r) kr += kc[r] * rt[r];
+      const R pnv = (ql + atp) + kr;
+      sync();  // every lane has read p_{k+1}
+      if (ln < 8) pv[ln] = pnv;
+      sync();
     };
-    // the stored r_k do not depend on the recursion: stage k-1's are fetched while stage k
-    // is formed (two stages per trip, alternating register sets; clamped fetches)
-    R rA[6], rB[6];
-    auto fetch = [&](R (&ro)[6], int ks) {
+    // the stored r_k and K columns do not depend on the recursion: stage k-1's are fetched
+    // while stage k is formed (two stages per trip, alternating register sets; clamped
+    // fetches)
+    R rA[6], rB[6], kA[6], kB[6];
+    auto fetch = [&](R (&ro)[6], R (&ko)[6], int ks) {
       const int kc = ks > 0 ? ks : 0;
 #pragma unroll
       for (int r = 0; r < 6; ++r) ro[r] = (R)rv[kc * 6 + r];
+#pragma unroll
+      for (int r = 0; r < 6; ++r) ko[r] = (R)Kl[kc * 48 + r * 8];
     };
-    if constexpr (CAP::deep) {
-      fetch(rA, N - 1);
-      for (int k = N - 1; k >= 0; k -= 2) {
-        fetch(rB, k - 1);
-        stage(k, rA);
-        if (k == 0) break;
-        fetch(rA, k - 2);
-        stage(k - 1, rB);
-      }
-    } else {
-      (void)rB;
-      for (int k = N - 1; k >= 0; --k) {
-        fetch(rA, k);
-        stage(k, rA);
-      }
+    fetch(rA, kA, N - 1);
+    for (int k = N - 1; k >= 0; k -= 2) {
+      fetch(rB, kB, k - 1);
+      stage(k, rA, kA);
+      if (k == 0) break;
+      fetch(rA, kA, k - 2);
+      stage(k - 1, rB, kB);
     }
     // k_k = -R~_k^-1 r~_k, lane k: R~_k's Cholesky factor and the two triangular solves
     if (ln < N) {
