@@ -78,6 +78,7 @@ struct Lay {
   int U, Ut, dU, dU2, zl, zu, xl, xu, sigx, ru, rres, dUr;
   int s, y, vl, vu, d, dt, ds, ds2, dc, dl, du, dms, filt;
   int gl, Hl, Qs, K, Rk;        // stage data / Riccati factors (global copies)
+  int tc;                       // transcendental values of the latest rollouts / stage costs (2 x 12 x NS)
   // restoration phase: reference/backup iterate, p/n and their multipliers, steps, filter
   int UR, zl0, zu0, s0, vl0, vu0, pR, nR, zpR, znR, dpR, dnR, dyR, dp2R, dn2R, dy2R, cms, filtR;
   int accU, accZl, accZu, accY;  // last acceptable iterate (BacktrackingLineSearch::StoreAcceptablePoint)
@@ -140,6 +141,7 @@ constexpr Lay make_layout(int N, int m, bool lr, bool refine, bool eq) {
     L.eqy = g; g += al8(ng); L.eqy2 = g; g += al8(ng); L.weqy = g; g += al8(ng);
   }
   if (!lr) { L.kf = g; g += al8(6 * N); }
+  L.tc = g; g += al8(2 * 12 * NS);
   L.wstotal = g;
   L.X = o; o += al2(nX); L.Xt = o; o += al2(nX); L.dX = o; o += al2(nX);
   L.trig = o; o += al2(8 * NS); L.qs = o; o += al2(10 * NS); L.lam = o; o += al2(8 * NS);
@@ -341,8 +343,12 @@ enum Phase { PH_ROLLOUT, PH_EVAL, PH_DERIVS, PH_ADJ, PH_SUMM, PH_RIC, PH_RESOLVE
 #define STAMPV0(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
 #define STAMPV1(v, ph) do { const unsigned long long _tv1 = __builtin_amdgcn_s_memtime(); \
     if (lanef() == 0) stamps[ph] += (double)(_tv1 - v); } while (0)
+#ifndef NMPC_XSTAMPS
 #define STAMP1(ph) do { const unsigned long long _ts1 = __builtin_amdgcn_s_memtime(); \
     if (lanef() == 0) stamps[ph] += (double)(_ts1 - _ts0); } while (0)
+#else
+#define STAMP1(ph) do { (void)_ts0; } while (0)
+#endif
 #else
 #define STAMP0() do {} while (0)
 #define STAMP1(ph) do {} while (0)
@@ -364,6 +370,21 @@ enum Phase { PH_ROLLOUT, PH_EVAL, PH_DERIVS, PH_ADJ, PH_SUMM, PH_RIC, PH_RESOLVE
 #ifndef NMPC_STAMPS
 #define STAMPV0(v) do {} while (0)
 #define STAMPV1(v, ph) do {} while (0)
+#endif
+// -DNMPC_XSTAMPS (diagnostics, with NMPC_STAMPS): the generic phase timers are off and the
+// slots record the parts of a restoration iteration instead (scripts/chain_xphases.py;
+// slots 14, 15, 17, 18 keep their generic meaning)
+enum XPhase { X_TCTRL = 0, X_TROLL = 1, X_TEVAL = 2, X_TROWS = 3, X_TFIN = 4, X_TCNT = 5, X_SCMS = 6,
+              X_SASM = 7, X_SRES = 8, X_SFWD = 9, X_SBLK = 10, X_NASM = 11, X_NRIC = 12, X_NFIN = 13,
+              X_CONV = 16, X_ACC = 19, X_DER = 20, X_LS = 21, X_IT = 22, X_ICNT = 23 };
+#if defined(NMPC_STAMPS) && defined(NMPC_XSTAMPS)
+#define XSTAMP0(v) STAMPV0(v)
+#define XSTAMP1(v, ph) STAMPV1(v, ph)
+#define XCOUNT(ph) do { if (lanef() == 0) stamps[ph] += 1.0; } while (0)
+#else
+#define XSTAMP0(v) do {} while (0)
+#define XSTAMP1(v, ph) do {} while (0)
+#define XCOUNT(ph) do {} while (0)
 #endif
 
 template <class CAP>
@@ -446,6 +467,14 @@ struct Solver {
   RV *dl, *du;  // row bounds: LDS or global with the rows (Cap::lds_rows)
   LDS double* rvars;
   GLB double* gl, *Hl, *Qs;
+  // The transcendental values a trial's rollout and stage costs form at its states (per
+  // stage: cos/sin theta, cos/sin psi, the four FOV tangents, cos/sin x7, the target
+  // distance), two buffers: trial group 0 (every single rollout / eval_fg) and group 1 (the
+  // second trial of a speculative pair).  The derivatives at an accepted trial point read
+  // them instead of evaluating them again (Solver::derivs<.., true>): the same functions of
+  // the same doubles, so the same values.
+  GLB double* tc;
+  static constexpr int TCS = 12 * (CAP::nmax + 1);
   LDS double* trig, *qs, *lam;
   GLB double* K, *Rk;
   using KFT = std::conditional_t<CAP::lds_rows, LDS double, GLB double>;
@@ -495,7 +524,7 @@ struct Solver {
     wU = gw + L.wU; wzl = gw + L.wzl; wzu = gw + L.wzu; wdU = gw + L.wdU; wsl = gw + L.ws; wy = gw + L.wy;
     wvl = gw + L.wvl; wvu = gw + L.wvu; wds = gw + L.wds; wpR = gw + L.wpR; wnR = gw + L.wnR;
     wzpR = gw + L.wzpR; wznR = gw + L.wznR; wdpR = gw + L.wdpR; wdnR = gw + L.wdnR; wdyR = gw + L.wdyR;
-    gl = gw + L.gl; Hl = gw + L.Hl; trig = sm + L.trig; Qs = gw + L.Qs; qs = sm + L.qs;
+    gl = gw + L.gl; Hl = gw + L.Hl; tc = gw + L.tc; trig = sm + L.trig; Qs = gw + L.Qs; qs = sm + L.qs;
     lam = sm + L.lam;
     K = gw + L.K; Rk = gw + L.Rk; Rc = sm + L.Rc; Rv = sm + L.Rv;
     if constexpr (CAP::lds_rows) kf = (KFT*)(sm + L.kf);
@@ -550,11 +579,15 @@ struct Solver {
           for (int c = 0; c < 5; ++c) a[c] = a[c] + inc[j * 8 + c];
         }
       }
-      if (k < N) {
+      {  // (stage N too: its trig goes to the cache only)
         const double ct = cos(a[0]), st_ = sin(a[0]), cp = cos(a[1]), sp = sin(a[1]);
-        inc[k * 8 + 5] = T * (v * cp * ct);
-        inc[k * 8 + 6] = T * (v * sp * ct);
-        inc[k * 8 + 7] = T * (v * st_);
+        if (k < N) {
+          inc[k * 8 + 5] = T * (v * cp * ct);
+          inc[k * 8 + 6] = T * (v * sp * ct);
+          inc[k * 8 + 7] = T * (v * st_);
+        }
+        GLB double* tk = tc + k * 12;
+        tk[0] = ct; tk[1] = st_; tk[2] = cp; tk[3] = sp;
       }
     }
     sync();
@@ -587,23 +620,28 @@ struct Solver {
   // ---------------------------------------------------------- stage cost value
   // Literal restatement of NMPC_TT.py:209-220 (same operation order as the
   // oracle's stage_cost).
-  __device__ __forceinline__ double stage_cost(const LDS double* x) const {
+  // (tw non-null: the tangents, cos/sin x7 and the target distance also go to the cache)
+  __device__ __forceinline__ double stage_cost(const LDS double* x, GLB double* tw = nullptr) const {
     const double hv = P->hv, hh = P->hh;
     const double z = x[2];
-    const double a = (z * tan(x[6] + hv) - z * tan(x[6] - hv)) / 2;
-    const double bb = (z * tan(x[5] + hh) - z * tan(x[5] - hh)) / 2;
+    const double t6p = tan(x[6] + hv), t6m = tan(x[6] - hv), t5p = tan(x[5] + hh), t5m = tan(x[5] - hh);
+    const double a = (z * t6p - z * t6m) / 2;
+    const double bb = (z * t5p - z * t5m) / 2;
     const double c7 = cos(x[7]), s7 = sin(x[7]);
     const double a2 = a * a, b2 = bb * bb;
     const double A = (c7 * c7) / a2 + (s7 * s7) / b2;
     const double Bq = 2 * c7 * s7 * ((1 / a2) - (1 / b2));
     const double C = (s7 * s7) / a2 + (c7 * c7) / b2;
-    const double XE = x[0] + a + z * tan(x[6] - hv);
-    const double YE = x[1] + bb + z * tan(x[5] - hh);
+    const double XE = x[0] + a + z * t6m;
+    const double YE = x[1] + bb + z * t5m;
     const double xt = pp[8], yt = pp[9];
     const double ex = xt - XE, ey = yt - YE;
     const double dx = x[0] - xt, dy = x[1] - yt;
-    return rvars[30] * sqrt(dx * dx + dy * dy) +
-           rvars[31] * ((A * (ex * ex) + Bq * ey * ex + C * (ey * ey)) - 1);
+    const double dd = sqrt(dx * dx + dy * dy);
+    if (tw) {
+      tw[4] = t6p; tw[5] = t6m; tw[6] = t5p; tw[7] = t5m; tw[8] = c7; tw[9] = s7; tw[10] = dd;
+    }
+    return rvars[30] * dd + rvars[31] * ((A * (ex * ex) + Bq * ey * ex + C * (ey * ey)) - 1);
   }
 
   __device__ __forceinline__ double row_value(const LDS double* x, int i) const {
@@ -621,7 +659,7 @@ struct Solver {
     double f = 0.0;
     if (k <= N) {
       const LDS double* xk = Xs + k * 8;
-      if (k < N) f = stage_cost(xk);
+      if (k < N) f = stage_cost(xk, tc + k * 12);
       if constexpr (!CAP::deep) {  // register-limited classes: one row at a time (fewer live values)
 #pragma unroll
         for (int i = 0; i < CAP::mmax; ++i) {
@@ -680,6 +718,7 @@ struct Solver {
     const double a_ = grp ? a1 : a0;
     LDS double* ic = grp ? qs : inc;
     LDS double* Xd = grp ? lam : Xt;
+    GLB double* tcg = tc + (grp ? TCS : 0);
     auto uk = [&](int j) { return Us[j] + a_ * dUs[j]; };
     const double v = k < N ? uk(k * 6) : 0.0;
     if (k < N) {
@@ -698,11 +737,15 @@ struct Solver {
 #pragma unroll
         for (int c = 0; c < 5; ++c) a[c] = a[c] + ij[c];
       }
-      if (k < N) {
+      {
         const double ct = cos(a[0]), st_ = sin(a[0]), cp = cos(a[1]), sp = sin(a[1]);
-        ic[k * 8 + 5] = T * (v * cp * ct);
-        ic[k * 8 + 6] = T * (v * sp * ct);
-        ic[k * 8 + 7] = T * (v * st_);
+        if (k < N) {
+          ic[k * 8 + 5] = T * (v * cp * ct);
+          ic[k * 8 + 6] = T * (v * sp * ct);
+          ic[k * 8 + 7] = T * (v * st_);
+        }
+        GLB double* tk = tcg + k * 12;
+        tk[0] = ct; tk[1] = st_; tk[2] = cp; tk[3] = sp;
       }
     }
     sync();
@@ -731,7 +774,7 @@ struct Solver {
     double f = 0.0;
     if (k <= N) {
       const LDS double* xk = (grp ? lam : Xt) + k * 8;
-      if (k < N) f = stage_cost(xk);
+      if (k < N) f = stage_cost(xk, tc + (grp ? TCS : 0) + k * 12);
       const double x0 = xk[0], x1 = xk[1];
       double gv[CAP::mmax];
 #pragma unroll
@@ -765,15 +808,23 @@ struct Solver {
   // objective by 0 (hfac = 0 in its assembly, so Hl is never read there; its 0 * gl terms
   // keep the gradient's exact values); the full derivatives are formed again when it
   // returns to the original problem
-  template <bool HESS = true>
-  __device__ __forceinline__ void derivs(const LDS double* Xs, const GLB double* Us) {
+  // TC: the transcendental values come from the cache buffer tcr, written by the rollout and
+  // stage costs that formed Xs (the callers pass the buffer of the trial that became Xs)
+  template <bool HESS = true, bool TC = false>
+  __device__ __forceinline__ void derivs(const LDS double* Xs, const GLB double* Us,
+                                         const GLB double* tcr = nullptr) {
     STAMP0();
     const int k = lanef();
     if (k <= N) {
       const LDS double* xk = Xs + k * 8;
       const double th = xk[3], ps = xk[4];
       LDS double* tg = trig + k * 8;
-      tg[0] = cos(th); tg[1] = sin(th); tg[2] = cos(ps); tg[3] = sin(ps);
+      const GLB double* tk = TC ? tcr + k * 12 : nullptr;
+      if constexpr (TC) {
+        tg[0] = tk[0]; tg[1] = tk[1]; tg[2] = tk[2]; tg[3] = tk[3];
+      } else {
+        tg[0] = cos(th); tg[1] = sin(th); tg[2] = cos(ps); tg[3] = sin(ps);
+      }
       tg[4] = (k < N) ? Us[k * 6] : 0.0;
       GLB double* g8 = gl + k * 8;
       GLB double* H = Hl + k * 21;
@@ -785,8 +836,8 @@ struct Solver {
         const double hv = P->hv, hh = P->hh;
         const double x = xk[0], yy = xk[1], z = xk[2], x5 = xk[5], x6 = xk[6], x7 = xk[7];
         const double xt = pp[8], yt = pp[9];
-        const double t6p = tan(x6 + hv), t6m = tan(x6 - hv);
-        const double t5p = tan(x5 + hh), t5m = tan(x5 - hh);
+        const double t6p = TC ? tk[4] : tan(x6 + hv), t6m = TC ? tk[5] : tan(x6 - hv);
+        const double t5p = TC ? tk[6] : tan(x5 + hh), t5m = TC ? tk[7] : tan(x5 - hh);
         const double al6 = (t6p - t6m) / 2, be6 = (t6p + t6m) / 2;
         const double al5 = (t5p - t5m) / 2, be5 = (t5p + t5m) / 2;
         const double al6d = (t6p * t6p - t6m * t6m) / 2, be6d = (2 + t6p * t6p + t6m * t6m) / 2;
@@ -802,7 +853,7 @@ struct Solver {
         const double a = z * al6, bb = z * al5;
         double ga[6] = {0.0, 0.0, al6, 0.0, z * al6d, 0.0};
         double gb[6] = {0.0, 0.0, al5, z * al5d, 0.0, 0.0};
-        const double c = cos(x7), sn = sin(x7);
+        const double c = TC ? tk[8] : cos(x7), sn = TC ? tk[9] : sin(x7);
         const double r1 = c * ex + sn * ey;
         const double r2 = sn * ex - c * ey;
         double u1[6], u2[6], gr1[6], gr2[6], ge1[6], ge2[6];
@@ -818,7 +869,7 @@ struct Solver {
           ge2[q] = (gr2[q] - e2 * gb[q]) * ib;
         }
         const double ddx = x - xt, ddy = yy - yt;
-        const double dd = sqrt(ddx * ddx + ddy * ddy);
+        const double dd = TC ? tk[10] : sqrt(ddx * ddx + ddy * ddy);
         const double idd = 1.0 / dd;
         const double id3 = idd * idd * idd;
         const double w1 = rvars[30], w2 = rvars[31];  // this scenario's cost weights
@@ -2357,6 +2408,8 @@ struct Solver {
     // accumulator keeps the per-lane order of barrier_obj / resto_pn_terms)
     RSTAMP0(_trs);
     RCOUNT(PH_DFTB);
+    XCOUNT(X_TCNT);
+    XSTAMP0(_x0);
     double th = 0.0, logs = 0.0, damp = 0.0, pn = 0.0, lg = 0.0, prox = 0.0;
     ctrls([&](int i, bool on) {
       const double ui = U[i] + a * dUs[i];
@@ -2367,6 +2420,7 @@ struct Solver {
       if (on) prox += pv;
     });
     sync();
+    XSTAMP1(_x0, X_TCTRL);
     bool bad = false;
     // theta_R, the barrier sums and the p/n sums in one pass over the rows
     auto rowpass = [&](auto dtv) {
@@ -2387,29 +2441,45 @@ struct Solver {
     if constexpr (kSpec) {
       if (spec == 2) {
         fo = *fo2;
+        XSTAMP0(_x3);
         rowpass(dms);
+        XSTAMP1(_x3, X_TROWS);
         done = true;
       } else if (spec == 1) {
+        XSTAMP0(_x1);
         rollout2(U, dUs, a, a2);
+        XSTAMP1(_x1, X_TROLL);
+        XSTAMP0(_x2);
         double f0, f1;
         eval_fg2(f0, f1);
         fo = df * f0;
         *fo2 = df * f1;
+        XSTAMP1(_x2, X_TEVAL);
+        XSTAMP0(_x3);
         rowpass(dt);
+        XSTAMP1(_x3, X_TROWS);
         done = true;
       }
     }
     if (!done) {
+      XSTAMP0(_x1);
       rollout(U, Xt, dUs, a);
+      XSTAMP1(_x1, X_TROLL);
+      XSTAMP0(_x2);
       fo = df * eval_fg(Xt, dt, dc);
+      XSTAMP1(_x2, X_TEVAL);
+      XSTAMP0(_x3);
       rowpass(dt);
+      XSTAMP1(_x3, X_TROWS);
     }
+    XSTAMP0(_x4);
     tht = wsum(th);
     if (wany(bad)) return false;
     const double phb = barrier_fin(0.0, logs, damp);
     pn = wsum(pn); lg = wsum(lg); prox = wsum(prox);
     rvars[34] = pn; rvars[35] = lg; rvars[36] = prox;
     phit = phb + pn_of(pn, lg, prox);
+    XSTAMP1(_x4, X_TFIN);
     RSTAMP1(_trs, PH_BARR);
     return isfinite(phit);
   }
@@ -2737,6 +2807,7 @@ __device__ __forceinline__ void resto_phase(const Params* __restrict__ prm, doub
       // storage, which is idle while restoration runs
       int rwd_cnt = 0, rwd_trial = 0;
       bool rin_wd = false;
+      int tcb_last = -1;  // the cache buffer of the current iterate's trial (-1: none, the entry point)
       volatile LDS double* WD = S.rvars + 40;
       auto lanef = [&]() { return S.lanef(); };  // for the STAMP macros
       (void)lanef;
@@ -2744,6 +2815,9 @@ __device__ __forceinline__ void resto_phase(const Params* __restrict__ prm, doub
       (void)stamps;
       while (true) {
         STAMP0();
+        XSTAMP0(_xit);
+        XCOUNT(X_ICNT);
+        XSTAMP0(_xcv);
         // after the first restoration iteration rvars[32..36] hold the sums of the
         // accepted trial, i.e. of the current iterate (p, n, s, U updated bit for bit)
         const bool cachedR = !firstR;
@@ -2894,6 +2968,7 @@ __device__ __forceinline__ void resto_phase(const Params* __restrict__ prm, doub
           S.etaR = o.resto_proximity_weight * sqrt(V[4]);
         }
         STAMP1(PH_CONV);
+        XSTAMP1(_xcv, X_CONV);
         // ---- Newton step of the restoration problem (p, n eliminated per row)
         { STAMP0();
         const double muR4 = V[4];  // volatile LDS scalar read once
@@ -2913,8 +2988,13 @@ __device__ __forceinline__ void resto_phase(const Params* __restrict__ prm, doub
         bool fok = false;
         while (true) {
           S.delta = dR;
+          XSTAMP0(_xa);
           S.assemble(SUM_RESTO, 0.0, 0.0, true);
-          if (S.riccati(S.sigx, S.ru)) { fok = true; break; }
+          XSTAMP1(_xa, X_NASM);
+          XSTAMP0(_xr);
+          const bool fact = S.riccati(S.sigx, S.ru);
+          XSTAMP1(_xr, X_NRIC);
+          if (fact) { fok = true; break; }
           sync();
           if (dR == 0.0) dR = (V[8] == 0.0) ? o.first_hessian_perturbation
                                               : fmax(o.min_hessian_perturbation, V[8] * o.perturb_dec_fact);
@@ -2925,6 +3005,7 @@ __device__ __forceinline__ void resto_phase(const Params* __restrict__ prm, doub
         V[9] = dR;
         S.delta = dR;
         if (!fok) { rstat = ST_STEP_ERR; break; }
+        XSTAMP0(_xnf);
         S.forward(S.dU, S.dX);
         S.refine(S.sigx, S.ru, S.dU, S.dX);
         // primal / dual fraction to the boundary of the Newton step, formed with its row pass
@@ -2954,6 +3035,7 @@ __device__ __forceinline__ void resto_phase(const Params* __restrict__ prm, doub
           rftb_d = wmin(ad);
           STAMP1(PH_ROWSTEP);
         }
+        XSTAMP1(_xnf, X_NFIN);
         V[17] = cachedR ? S.phi_of(0.0, S.rvars[32], S.rvars[33]) + S.pn_of(S.rvars[34], S.rvars[35], S.rvars[36])
                         : S.barrier_obj(0.0, S.U, S.s, nullptr, 0.0) + S.resto_pn_terms(S.U, 0.0, nullptr, nullptr);
         if (V[6] < 0) {
@@ -3023,7 +3105,7 @@ __device__ __forceinline__ void resto_phase(const Params* __restrict__ prm, doub
           sync();
           S.rollout(S.U, S.X);
           V[12] = S.df * S.eval_fg(S.X, S.d, S.dc);
-          S.template derivs<false>(S.X, S.U);
+          S.template derivs<false, true>(S.X, S.U, S.tc);
           V[15] = WD[0]; V[16] = WD[1]; V[17] = WD[2]; V[23] = 0.0;
           S.delta = WD[5];
           rwd_dir = true;
@@ -3032,8 +3114,10 @@ __device__ __forceinline__ void resto_phase(const Params* __restrict__ prm, doub
           rwd_cnt = 0;
         };
         STAMPV0(_tls);
+        XSTAMP0(_xls);
         V[19] = 0.0; V[20] = 0.0; V[21] = 0.0;
         int acc = 0, nsteps = 0;  // acc: 1 regular step, 2 SOC step
+        int tcb_acc = 0;  // the transcendental-cache buffer of the accepted trial (1: a pair's second)
         double a = 0.0, a_test = 0.0;
         bool rskip = false, rforced = false;
        while (true) {
@@ -3078,6 +3162,7 @@ __device__ __forceinline__ void resto_phase(const Params* __restrict__ prm, doub
           }
           if (ok_t && r_check(a, ph, th)) {
             acc = 1; V[19] = a; V[20] = fo_t; V[21] = ph; a_test = a;
+            tcb_acc = from_pair ? 1 : 0;
             if (from_pair) {  // the accepted trial's X and rows into Xt / dt for the accept
               if (S.lanef() <= N) {
 #pragma unroll
@@ -3093,6 +3178,7 @@ __device__ __forceinline__ void resto_phase(const Params* __restrict__ prm, doub
           }
           if (ok_t && a == V[18] && V[15] <= th && o.max_soc > 0) {
             RSTAMP0(_soc);
+            XSTAMP0(_xsb);
             double th_tr = th, th_old = 0.0, a_soc = a;
             for (int r = S.lanef(); r < ng; r += WAVE) S.cms[r] = S.d[r] - S.s[r] - S.pR[r] + S.nR[r];
             sync();
@@ -3102,15 +3188,23 @@ __device__ __forceinline__ void resto_phase(const Params* __restrict__ prm, doub
             bool soc_ok = false;
             while (cnt < o.max_soc && (cnt == 0 || th_tr <= o.kappa_soc * th_old)) {
               th_old = th_tr;
+              XSTAMP0(_xs1);
               for (int r = S.lanef(); r < ng; r += WAVE) {
                 const double sv = S.s[r] + a_soc * dsp[r], pv = S.pR[r] + a_soc * dpp[r], nv = S.nR[r] + a_soc * dnp[r];
                 S.cms[r] = a_soc * S.cms[r] + (S.dt[r] - sv - pv + nv);
               }
               sync();
+              XSTAMP1(_xs1, X_SCMS);
+              XSTAMP0(_xs2);
               S.assemble(SUM_RESTO_SOC, 0.0, 0.0, true);
+              XSTAMP1(_xs2, X_SASM);
+              XSTAMP0(_xs3);
               S.resolve(S.ru);
+              XSTAMP1(_xs3, X_SRES);
+              XSTAMP0(_xs4);
               S.forward(S.dU2, S.dX);
               S.refine(S.sigx, S.ru, S.dU2, S.dX);
+              XSTAMP1(_xs4, X_SFWD);
               double t0, t1;
               double ap, u1;
               const double tauR = V[5];
@@ -3132,6 +3226,7 @@ __device__ __forceinline__ void resto_phase(const Params* __restrict__ prm, doub
               th_tr = th2;
             }
             RSTAMP1(_soc, PH_FTB);
+            XSTAMP1(_xsb, X_SBLK);
             if (soc_ok) break;
           }
           a *= o.alpha_red_factor;
@@ -3140,11 +3235,13 @@ __device__ __forceinline__ void resto_phase(const Params* __restrict__ prm, doub
         break;
        }
         STAMPV1(_tls, PH_INIT);
+        XSTAMP1(_xls, X_LS);
         if (acc == 0) { rstat = ST_RESTO_FAIL; break; }  // no restoration inside the restoration phase
         rwd_cnt = (nsteps == 0) ? 0 : rwd_cnt + 1;
         // filter augmentation (F-type + Armijo steps do not augment)
         {
           STAMP0();
+          XSTAMP0(_xac);
           const GLB double* dUa = (acc == 2) ? S.dU2 : S.dU;
           const auto* dsa = (acc == 2) ? S.ds2 : S.ds;
           const GLB double* dpa = (acc == 2) ? S.dp2R : S.dpR;
@@ -3214,7 +3311,11 @@ __device__ __forceinline__ void resto_phase(const Params* __restrict__ prm, doub
           sync();
           V[12] = V[20];
           STAMP1(PH_ACCEPT);
-          S.template derivs<false>(S.X, S.U);
+          XSTAMP1(_xac, X_ACC);
+          XSTAMP0(_xde);
+          S.template derivs<false, true>(S.X, S.U, S.tc + tcb_acc * Solver<CAP>::TCS);
+          tcb_last = tcb_acc;
+          XSTAMP1(_xde, X_DER);
           ++it;
           if (trace && S.lanef() == 0) {
             double th = 0.0;
@@ -3225,6 +3326,7 @@ __device__ __forceinline__ void resto_phase(const Params* __restrict__ prm, doub
           }
           sync();
         }
+        XSTAMP1(_xit, X_IT);
       }
       S.filt = ofilt;
       S.nfilt = onf;
@@ -3235,7 +3337,8 @@ __device__ __forceinline__ void resto_phase(const Params* __restrict__ prm, doub
       if (rstat != 0) return;
       // back to the original problem: its objective's Hessian at the current iterate (the
       // restoration iterations formed the gradient only)
-      S.derivs(S.X, S.U);
+      if (tcb_last >= 0) S.template derivs<true, true>(S.X, S.U, S.tc + tcb_last * Solver<CAP>::TCS);
+      else S.derivs(S.X, S.U);
       // ---- back to the original problem: bound multipliers by a Newton step for
       //      complementarity over the whole restoration (fraction to the boundary,
       //      reset to 1 above bound_mult_reset_threshold); y = 0 (constr_mult_reset_threshold)
@@ -3406,7 +3509,7 @@ __device__ __forceinline__ int solve_one(Solver<CAP>& S, const Params* __restric
   if (status == 0) {
     S.rollout(S.U, S.X);
     const double F0 = S.eval_fg(S.X, S.d, nullptr);
-    S.derivs(S.X, S.U);
+    S.template derivs<true, true>(S.X, S.U, S.tc);
     S.adjoint(1.0, (const GLB double*)nullptr);
     double gmax = 0.0;
     bool bad = !isfinite(F0);
@@ -3497,7 +3600,7 @@ __device__ __forceinline__ int solve_one(Solver<CAP>& S, const Params* __restric
     sync();
     S.rollout(S.U, S.X);
     S.eval_fg(S.X, S.d, S.dc);
-    S.derivs(S.X, S.U);
+    S.template derivs<true, true>(S.X, S.U, S.tc);
     const double skp = o.slack_bound_push, skf = o.slack_bound_frac;
     for (int r = S.lanef(); r < ng; r += WAVE) {
       const double lo = S.dl[r], hi = S.du[r];
@@ -3861,7 +3964,7 @@ __device__ __forceinline__ int solve_one(Solver<CAP>& S, const Params* __restric
       sync();
       S.rollout(S.U, S.X);
       f = S.df * S.eval_fg(S.X, S.d, S.dc);
-      S.derivs(S.X, S.U);
+      S.template derivs<true, true>(S.X, S.U, S.tc);
       S.adjoint(S.df, S.y);  // grad of the Lagrangian there (soft restoration's pd error)
       theta_ref = WD[0]; phi_ref = WD[1]; gbd = WD[2];
       PW[0] = 0.0;
@@ -3935,7 +4038,7 @@ __device__ __forceinline__ int solve_one(Solver<CAP>& S, const Params* __restric
         S.dms[r] = S.y[r] + a * (S.eqr(r) ? S.eqy_()[r] : D * S.ds[r] + rs);  // trial y
       }
       sync();
-      S.derivs(S.Xt, S.Ut);
+      S.template derivs<true, true>(S.Xt, S.Ut, S.tc);
       // adjoint at the trial point: swap X temporarily
       LDS double* Xs = S.X; S.X = S.Xt;
       S.adjoint(S.df, S.dms);
@@ -4168,7 +4271,7 @@ __device__ __forceinline__ int solve_one(Solver<CAP>& S, const Params* __restric
       f = f_acc;
       phic = true;  // no barrier_obj call between the accepted trial and the next phi_ref
       STAMP1(PH_ACCEPT);
-      if (!derivs_done) S.derivs(S.X, S.U);
+      if (!derivs_done) S.template derivs<true, true>(S.X, S.U, S.tc);  // the accepted trial: the last one formed
       else {
         // soft resto computed derivatives at the trial; trig uses U (same values)
         sync();
