@@ -546,16 +546,32 @@ struct Solver {
   // Each lanef() k sums the increments j<k in order, i.e. bitwise the sequential
   // recursion; the (x,y,z) increments need theta_j, psi_j, so two passes.
   // (dUs non-null: the controls are Us + a dUs, formed here from the two vectors rather
-  // than read back from the trial point just stored -- the same doubles)
+  // than read back from the trial point just stored -- the same doubles; pre non-null: the
+  // two vectors' stage entries were loaded ahead by preload_u)
+  struct UPre { double u[6], du[6]; };
+  // a trial's stage controls loaded ahead, so the trial's rollout does not start by waiting
+  // on them (issued before the trial's control pass): lane l holds stage (l & kmask)'s
+  // entries of Us and dUs (clamped stage: no lane-dependent branch)
+  __device__ __forceinline__ UPre preload_u(const GLB double* Us, const GLB double* dUs, int kmask) const {
+    UPre q;
+    const int k = lanef() & kmask;
+    const int kc = k < N ? k : 0;
+#pragma unroll
+    for (int c = 0; c < 6; ++c) { q.u[c] = Us[kc * 6 + c]; q.du[c] = dUs[kc * 6 + c]; }
+    return q;
+  }
   __device__ __forceinline__ void rollout(const GLB double* Us, LDS double* Xd, const GLB double* dUs = nullptr,
-                                          double a_ = 0.0) {
+                                          double a_ = 0.0, const UPre* pre = nullptr) {
     STAMP0();
     const int k = lanef();
-    auto uk = [&](int j) { return dUs ? Us[j] + a_ * dUs[j] : Us[j]; };
-    const double v = k < N ? uk(k * 6) : 0.0;
+    auto uk = [&](int c) {  // stage k's control c
+      const int j = k * 6 + c;
+      return pre ? pre->u[c] + a_ * pre->du[c] : (dUs ? Us[j] + a_ * dUs[j] : Us[j]);
+    };
+    const double v = k < N ? uk(0) : 0.0;
     if (k < N) {
 #pragma unroll
-      for (int c = 0; c < 5; ++c) inc[k * 8 + c] = T * uk(k * 6 + 1 + c);
+      for (int c = 0; c < 5; ++c) inc[k * 8 + c] = T * uk(1 + c);
     }
     if (kUnrollStages && k < 8) inc[kZeroRow * 8 + k] = -0.0;
     sync();
@@ -711,7 +727,8 @@ struct Solver {
   // sits in lanes 32..63 -- the butterfly reduces each 32-lane half in the same order, so
   // both objectives are bitwise those of two separate calls.
   static constexpr bool kSpec = CAP::lds_rows && !CAP::refine && !CAP::eq && CAP::nmax <= 31;
-  __device__ __forceinline__ void rollout2(const GLB double* Us, const GLB double* dUs, double a0, double a1) {
+  __device__ __forceinline__ void rollout2(const GLB double* Us, const GLB double* dUs, double a0, double a1,
+                                           const UPre* pre = nullptr) {
     STAMP0();
     const int l = lanef();
     const int grp = l >> 5, k = l & 31;
@@ -719,11 +736,14 @@ struct Solver {
     LDS double* ic = grp ? qs : inc;
     LDS double* Xd = grp ? lam : Xt;
     GLB double* tcg = tc + (grp ? TCS : 0);
-    auto uk = [&](int j) { return Us[j] + a_ * dUs[j]; };
-    const double v = k < N ? uk(k * 6) : 0.0;
+    auto uk = [&](int c) {  // stage k's control c
+      const int j = k * 6 + c;
+      return pre ? pre->u[c] + a_ * pre->du[c] : Us[j] + a_ * dUs[j];
+    };
+    const double v = k < N ? uk(0) : 0.0;
     if (k < N) {
 #pragma unroll
-      for (int c = 0; c < 5; ++c) ic[k * 8 + c] = T * uk(k * 6 + 1 + c);
+      for (int c = 0; c < 5; ++c) ic[k * 8 + c] = T * uk(1 + c);
     }
     if (k < 8) ic[kZeroRow * 8 + k] = -0.0;
     sync();
@@ -2410,6 +2430,8 @@ struct Solver {
     RCOUNT(PH_DFTB);
     XCOUNT(X_TCNT);
     XSTAMP0(_x0);
+    UPre up;  // (a pair's second trial forms no rollout)
+    if (spec != 2) up = preload_u(U, dUs, (kSpec && spec == 1) ? 31 : WAVE - 1);
     double th = 0.0, logs = 0.0, damp = 0.0, pn = 0.0, lg = 0.0, prox = 0.0;
     ctrls([&](int i, bool on) {
       const double ui = U[i] + a * dUs[i];
@@ -2447,7 +2469,7 @@ struct Solver {
         done = true;
       } else if (spec == 1) {
         XSTAMP0(_x1);
-        rollout2(U, dUs, a, a2);
+        rollout2(U, dUs, a, a2, &up);
         XSTAMP1(_x1, X_TROLL);
         XSTAMP0(_x2);
         double f0, f1;
@@ -2463,7 +2485,7 @@ struct Solver {
     }
     if (!done) {
       XSTAMP0(_x1);
-      rollout(U, Xt, dUs, a);
+      rollout(U, Xt, dUs, a, &up);
       XSTAMP1(_x1, X_TROLL);
       XSTAMP0(_x2);
       fo = df * eval_fg(Xt, dt, dc);
@@ -2665,6 +2687,7 @@ struct Solver {
   __device__ __forceinline__ bool trial(double a, const GLB double* dUs, const RV* dss, double& ft, double& phit,
                         double& tht) {
     // the trial controls and their barrier terms in one pass
+    const UPre up = preload_u(U, dUs, WAVE - 1);
     double th = 0.0, logs = 0.0, damp = 0.0;
     ctrls([&](int i, bool on) {
       const double ui = U[i] + a * dUs[i];
@@ -2672,7 +2695,7 @@ struct Solver {
       barrier_ctrl1(i, on, ui, logs, damp);
     });
     sync();
-    rollout(U, Xt, dUs, a);
+    rollout(U, Xt, dUs, a, &up);
     ft = df * eval_fg(Xt, dt, dc);
     // theta and the barrier sums in one pass over the rows
     bool bad = false;
