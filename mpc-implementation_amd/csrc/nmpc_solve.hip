@@ -1031,30 +1031,38 @@ struct Solver {
       for (int q = 0; q < 6; ++q) lam[k * 8 + cs[q]] = acc[q];
     }
     sync();
+    // stage j's terms of the theta / psi recursion, ((E03 l0 + E13 l1) + E23 l2) and
+    // (E04 l0 + E14 l1) with l = lam_{j+1}: formed once, by lane j, into the w slots 5 and 6
+    // (dead after the suffix sums), instead of by every lane for every stage -- the same
+    // expressions, so the same bits
+    if (k < N) {
+      double E03, E04, E13, E14, E23, b00, b10, b20;
+      stage_AB(k, E03, E04, E13, E14, E23, b00, b10, b20);
+      const LDS double* ln = lam + (k + 1) * 8;
+      wv[k * 8 + 5] = (E03 * ln[0] + E13 * ln[1]) + E23 * ln[2];
+      wv[k * 8 + 6] = E04 * ln[0] + E14 * ln[1];
+    }
+    sync();
     if (k <= N) {
       double a3 = wv[N * 8 + 3], a4 = wv[N * 8 + 4];
       if constexpr (kUnrollStages) {
-        // every lane evaluates each stage term (clamped stage index: valid reads, no
-        // lane-dependent branch) and keeps it only where its guard holds
+        // every lane reads each stage's terms (clamped stage index: valid reads, no
+        // lane-dependent branch) and keeps the sum only where its guard holds
 #pragma unroll
         for (int j = CAP::nmax - 1; j >= 0; --j) {
           const bool on = j < N && j >= k;
           const int jc = j < N ? j : 0;
-          double E03, E04, E13, E14, E23, b00, b10, b20;
-          stage_AB(jc, E03, E04, E13, E14, E23, b00, b10, b20);
-          const LDS double* ln = lam + (jc + 1) * 8;
-          const double n3 = wv[jc * 8 + 3] + (((E03 * ln[0] + E13 * ln[1]) + E23 * ln[2]) + a3);
-          const double n4 = wv[jc * 8 + 4] + ((E04 * ln[0] + E14 * ln[1]) + a4);
+          const LDS double* wj = wv + jc * 8;
+          const double n3 = wj[3] + (wj[5] + a3);
+          const double n4 = wj[4] + (wj[6] + a4);
           a3 = on ? n3 : a3;
           a4 = on ? n4 : a4;
         }
       } else {
         for (int j = N - 1; j >= k; --j) {
-          double E03, E04, E13, E14, E23, b00, b10, b20;
-          stage_AB(j, E03, E04, E13, E14, E23, b00, b10, b20);
-          const LDS double* ln = lam + (j + 1) * 8;
-          a3 = wv[j * 8 + 3] + (((E03 * ln[0] + E13 * ln[1]) + E23 * ln[2]) + a3);
-          a4 = wv[j * 8 + 4] + ((E04 * ln[0] + E14 * ln[1]) + a4);
+          const LDS double* wj = wv + j * 8;
+          a3 = wj[3] + (wj[5] + a3);
+          a4 = wj[4] + (wj[6] + a4);
         }
       }
       lam[k * 8 + 3] = a3;
