@@ -17,8 +17,9 @@ What "agreement" can mean here is measured, not assumed: tests/golden/gen_roundi
 re-solves every fixture step with solvers that differ from the fixture's by rounding alone --
 three variants of the oracle (the same Newton steps factored in a permuted variable order)
 and the compiled restatement (the same algorithm with the Riccati factorisation the kernel
-uses) -- and re-runs every whole loop with them (ref_run_<name>_spread.npz).  The fixture's x is not defined beyond rounding on the steps
-where those variants move it (flat optima, termination tests decided within rounding of
+uses) -- and re-runs every whole loop with them (ref_run_<name>_spread.npz).  The
+fixture's x is not defined beyond rounding on the steps where those variants move it
+(flat optima, termination tests decided within rounding of
 their threshold), and the closed loops are chaotic: rounding-level variants of the SAME
 solver part after some steps and end with different whole-run sums.
 
@@ -30,10 +31,10 @@ Three comparisons per run:
       count that differs at a step no variant moves is a one-iteration flip of a
       termination test -- both sides converged to the same x within 1e-6, or both
       infeasible, with the deciding check (the restoration NLP's own for infeasible steps)
-      passing on one side and missing tol by at most 100x on the other; at every step where the GPU's status or converged x differs, the
-      GPU's (status, x) lies in the rounding variants' envelope there (some variant's
-      status, and x within 1e-6 of that variant's or no farther from the fixture's than
-      that variant's); and the GPU changes
+      passing on one side and missing tol by at most 100x on the other; at every step
+      where the GPU's status or converged x differs, the GPU's (status, x) lies in the
+      rounding variants' envelope there (some variant's status, and x within 1e-6 of that
+      variant's or no farther from the fixture's than that variant's); and the GPU changes
       no more statuses than the variants and no more converged x than the compiled
       restatement does; measured regression floors besides.
       For every differing step the test prints which termination test decided and its
