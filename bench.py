@@ -95,7 +95,7 @@ def pmc_summary(kernel, steps, batch, warmup):
     return out
 
 
-def cpu_baseline(spec_cfg, cfg, P, lbx, ubx, lbg, ubg, K, W=0, p_step=None, budget_s=15.0):
+def cpu_baseline(spec_cfg, cfg, P, lbx, ubx, lbg, ubg, K, W=0, p_step=None, budget_s=15.0, cold=True):
     """Time the compiled CPU restatement (oracle/cpu_ipopt.cpp: C++/OpenMP, the same
     IPOPT restatement with a Riccati Newton step, pinned to the numpy oracle's
     fixtures by tests/test_cpu_restatement.py) on the bench's own workload and window:
@@ -145,6 +145,22 @@ def cpu_baseline(spec_cfg, cfg, P, lbx, ubx, lbg, ubg, K, W=0, p_step=None, budg
     its = np.concatenate([r["iter"][b, :done[b]] for b in rows]) if len(rows) else np.zeros(0)
     sts = np.concatenate([r["status"][b, :done[b]] for b in rows]) if len(rows) else np.zeros(0, int)
     tsv = np.concatenate([r["solve_s"][b, :done[b]] for b in rows]) if len(rows) else np.zeros(0)
+    def pct(v):
+        return {"p50_ms": float(np.percentile(v, 50) * 1e3), "p99_ms": float(np.percentile(v, 99) * 1e3),
+                "max_ms": float(v.max() * 1e3)} if len(v) else None
+    out = {"value": n / wall, "unit": "MPC steps/s", "cores": nthr, "kind": "port",
+           "sample": f"{n} warm-started closed-loop MPC steps (solve + shift) of the GPU's timed window -- "
+                     f"steps {W}..{W + K - 1} after the same {W} untimed warm-up steps, up to {K} per scenario, "
+                     f"{len(rows)} of the bench's config-{cfg} scenarios ({len(sel)} warmed within the budget) -- "
+                     f"by oracle/cpu_ipopt.cpp (CPU "
+                     f"restatement, not CasADi: C++/OpenMP IPOPT restatement with a Riccati step), "
+                     f"{nthr} threads, budget {budget_s:.0f}s, wall {wall:.1f}s",
+           "mean_ip_iterations": float(its.mean()) if n else None,
+           "iterations_per_s_per_core": float(its.sum() / wall / nthr) if n else None,
+           "per_solve_wall": pct(tsv),
+           "status_histogram": {int(k): int(v) for k, v in zip(*np.unique(sts, return_counts=True))}}
+    if not cold:
+        return out
     # cold-start leg (cold u = 0 and warm-started): every scenario's NLP of
     # the timed window's first step from u = 0, the same threads
     t1 = time.perf_counter()
@@ -152,25 +168,12 @@ def cpu_baseline(spec_cfg, cfg, P, lbx, ubx, lbg, ubg, K, W=0, p_step=None, budg
                                orc.REFERENCE_OPTS, threads=nthr)
     cwall = time.perf_counter() - t1
 
-    def pct(v):
-        return {"p50_ms": float(np.percentile(v, 50) * 1e3), "p99_ms": float(np.percentile(v, 99) * 1e3),
-                "max_ms": float(v.max() * 1e3)} if len(v) else None
     cold = {"value": P1.shape[0] / cwall, "unit": "NLP solves/s", "solves": int(P1.shape[0]), "wall_s": cwall,
             "mean_ip_iterations": float(rc["iter"].mean()), "per_solve_wall": pct(rc["solve_s"]),
             "status_histogram": {int(k): int(v) for k, v in zip(*np.unique(rc["status"], return_counts=True))},
             "sample": f"cold solves (u = 0) of the timed window's first step, {P1.shape[0]} scenarios, {nthr} threads"}
-    return {"value": n / wall, "unit": "MPC steps/s", "cores": nthr, "kind": "port",
-            "sample": f"{n} warm-started closed-loop MPC steps (solve + shift) of the GPU's timed window -- "
-                      f"steps {W}..{W + K - 1} after the same {W} untimed warm-up steps, up to {K} per scenario, "
-                      f"{len(rows)} of the bench's config-{cfg} scenarios ({len(sel)} warmed within the budget) -- "
-                      f"by oracle/cpu_ipopt.cpp (CPU "
-                      f"restatement, not CasADi: C++/OpenMP IPOPT restatement with a Riccati step), "
-                      f"{nthr} threads, budget {budget_s:.0f}s, wall {wall:.1f}s",
-            "mean_ip_iterations": float(its.mean()) if n else None,
-            "iterations_per_s_per_core": float(its.sum() / wall / nthr) if n else None,
-            "per_solve_wall": pct(tsv),
-            "status_histogram": {int(k): int(v) for k, v in zip(*np.unique(sts, return_counts=True))},
-            "cold_start": cold}
+    out["cold_start"] = cold
+    return out
 
 
 def parity_sample(solver, spec, start, K, records, bnd, dev, p_step=None, tol=1e-6):
@@ -292,6 +295,12 @@ def main():
     ap.add_argument("--in-order", action="store_true",
                     help="fused mode: dispatch scenarios in index order (no longest-first order)")
     ap.add_argument("--cpu-budget", type=float, default=20.0)
+    ap.add_argument("--no-config5", action="store_true",
+                    help="skip the config-5 side leg (N=50, 10 obstacles of which 6 move; N=1 only)")
+    ap.add_argument("--config5-batch", type=int, default=8192, help="config-5 leg: scenarios (BASELINE config 5)")
+    ap.add_argument("--config5-cpu-scenarios", type=int, default=2048,
+                    help="config-5 leg: scenarios in the CPU baseline's bounded sample")
+    ap.add_argument("--config5-cpu-budget", type=float, default=8.0)
     ap.add_argument("--dump-rows", default="",
                     help="fused mode: rank 0 saves the gathered (scenarios, 8K) per-step rows (u0, f, status) "
                          "of the timed launch to this .npy (multi-rank rehearsal test)")
@@ -309,9 +318,7 @@ def main():
 
     import torch
     import torch.distributed as dist
-    from nmpc_amd import nlpsol, config_spec, draw_scenarios, REFERENCE_OPTS
-    from nmpc_amd.dist import shard, pack_result, gather_rows, gather_closed_loop, pack_closed_loop
-    from nmpc_amd.schedule import longest_first
+    from nmpc_amd import config_spec, draw_scenarios
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -319,15 +326,19 @@ def main():
 
     spec = config_spec(args.config)
     B, K, W = args.batch, args.steps, args.warmup
-    cpu_res = None
-    ps_np = None
-    if spec.np > spec.np_min:  # moving obstacles (config 5), see pstep below
-        from nmpc_amd.targets import obstacle_steps
-        ps_np = obstacle_steps(195, W + K, spec.np)
+    # the config-5 side leg (BASELINE config 5, Dynamic Obstacle avoidance.m:211-231): N=1 only
+    leg5 = world == 1 and args.config != 5 and args.mode == "fused" and not args.no_config5
+    cpu_res = cpu5 = None
     if world == 1 and not args.no_cpu_baseline:  # OpenMP threads, before the GPU is initialised
         lb = spec.bounds()
         cpu_res = cpu_baseline(spec, args.config, draw_scenarios(spec, B, seed=1000 + args.config), *lb, K, W,
-                               p_step=ps_np, budget_s=args.cpu_budget)
+                               p_step=obstacle_pstep(spec, W + K), budget_s=args.cpu_budget)
+        cpu_res_start, cpu_res_records = cpu_baseline.start, cpu_baseline.records
+        if leg5:
+            s5 = config_spec(5)
+            cpu5 = cpu_baseline(s5, 5, draw_scenarios(s5, args.config5_batch, seed=1005)[:args.config5_cpu_scenarios],
+                                *s5.bounds(), K, W, p_step=obstacle_pstep(s5, W + K), budget_s=args.config5_cpu_budget,
+                                cold=False)
     # NMPC_BENCH_BACKEND=gloo rehearses the multi-rank path on one GPU (all ranks on
     # cuda:0); the measured configuration is one process per GPU over RCCL ("nccl")
     backend = os.environ.get("NMPC_BENCH_BACKEND", "nccl")
@@ -339,6 +350,64 @@ def main():
         else:
             dist.init_process_group(backend)
     dev = torch.device("cuda", dev_idx)
+    ctx = dict(world=world, rank=rank, backend=backend, dev=dev, dist=dist)
+
+    m = measure(args, ctx, args.config, B, K, W, args.mode, per_step_side=(args.mode == "fused" and not args.no_per_step),
+                dump_rows=args.dump_rows)
+    m5 = measure(args, ctx, 5, args.config5_batch, K, W, "fused", per_step_side=False) if leg5 else None
+
+    if rank == 0:
+        res = result_line(args, m, world)
+        if m["side"] is not None:
+            res["per_step_launch"] = m["side"]
+        if cpu_res is not None:
+            res["cpu_baseline"] = cpu_res
+            if world == 1 and cpu_res_records:
+                res["parity_sample"] = parity_sample(m["solver"], m["spec"], cpu_res_start, K, cpu_res_records,
+                                                     m["bnd"], dev, p_step=m["ps_np"][W:W + K] if m["ps_np"] is not None
+                                                     else None)
+        if m5 is not None:
+            r5 = result_line(args, m5, world)
+            leg = {k: r5[k] for k in ("value", "unit", "ms_per_step", "steps", "warmup", "config", "roofline",
+                                      "mean_ip_iterations", "status_histogram", "dispatch", "scheduler_error",
+                                      "steps_done") if k in r5}
+            leg["note"] = ("BASELINE config 5 (N=50, 10 obstacles of which 6 move per MATLAB/Dynamic Obstacles/"
+                           "Dynamic Obstacle avoidance.m:211-231), timed like the headline: W warm-up MPC steps, "
+                           "then K closed-loop steps per scenario in one launch (HIP events on the launch stream); "
+                           "a side leg, not the headline value")
+            if cpu5 is not None:
+                leg["cpu_baseline"] = cpu5
+            res["config5"] = leg
+        print(json.dumps(res))
+        if args.dump_rows and args.mode == "fused":
+            np.save(args.dump_rows, m["rows"].cpu().numpy())
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def obstacle_pstep(spec, n):
+    """Moving obstacles (config 5: MATLAB/Dynamic Obstacles/Dynamic Obstacle avoidance.m:213-230,
+    from MPC iteration 195 as in the config-5 fixtures; the W warm-up steps come first):
+    (n, np) per-step parameter increments, or None for a static layout."""
+    if spec.np <= spec.np_min:
+        return None
+    from nmpc_amd.targets import obstacle_steps
+    return obstacle_steps(195, n, spec.np)
+
+
+def measure(args, ctx, cfg, B, K, W, mode, per_step_side=False, dump_rows=""):
+    """One configuration on this rank's GPU: W warm-up MPC steps, then exactly K timed steps
+    bracketed by barrier + synchronize (fused: one launch, timed twice over -- once on scratch
+    copies of the same state, then the timed launch); HIP events on the launch stream give the
+    kernel time.  Returns the raw measurements."""
+    import torch
+    from nmpc_amd import nlpsol, config_spec, draw_scenarios, REFERENCE_OPTS
+    from nmpc_amd.dist import shard, pack_result, gather_rows, gather_closed_loop, pack_closed_loop
+    from nmpc_amd.schedule import longest_first
+
+    world, rank, backend, dev, dist = ctx["world"], ctx["rank"], ctx["backend"], ctx["dev"], ctx["dist"]
+    spec = config_spec(cfg)
+    ps_np = obstacle_pstep(spec, W + K)
 
     def all_reduce(t, op):
         if backend == "nccl":
@@ -348,7 +417,7 @@ def main():
             dist.all_reduce(h, op=op)
             t.copy_(h)
     # global scenario stream, sliced per rank (results independent of world size)
-    P_all = draw_scenarios(spec, B * world, seed=1000 + args.config)
+    P_all = draw_scenarios(spec, B * world, seed=1000 + cfg)
     P = P_all[shard(B * world, world, rank)]
     lbx, ubx, lbg, ubg = spec.bounds()
     solver = nlpsol("solver", "ipopt", spec, REFERENCE_OPTS)
@@ -361,8 +430,6 @@ def main():
     v_t = torch.full((B,), 12.0, **f64)   # target speed, Python/NMPC_TT.py:25
     w_t = torch.full((B,), 0.01, **f64)   # target turn rate
     stream = torch.cuda.current_stream()
-    # moving obstacles (config 5: MATLAB/Dynamic Obstacles/Dynamic Obstacle avoidance.m:213-230,
-    # from MPC iteration 195 as in the config-5 fixtures; the W warm-up steps come first)
     pstep = None if ps_np is None else torch.tensor(ps_np, **f64)
 
     def hist_bufs(k):
@@ -398,7 +465,7 @@ def main():
         if world > 1:  # the only exchange: final gather of every step's (u0, f, status)
             rows = gather_closed_loop(hist, world, total=B * world)
         else:
-            rows = pack_closed_loop(hist) if args.dump_rows else None
+            rows = pack_closed_loop(hist) if dump_rows else None
         if timed_events is not None:
             fused.rows = rows
 
@@ -448,109 +515,105 @@ def main():
         timed_run.chain = ht["iters"].sum(0).cpu().numpy()
         return float(el_t.item()), kern_ms, float(tot[0].item() / tot[1].item()), hist
 
-    elapsed, kern_ms, ibar, status_hist = timed_run(args.mode, p0.clone(), w0.clone())
-    fov_mean = timed_run.fov if args.mode == "fused" else None
-    side = None
-    if args.mode == "fused" and not args.no_per_step:
+    elapsed, kern_ms, ibar, status_hist = timed_run(mode, p0.clone(), w0.clone())
+    res = {"cfg": cfg, "spec": spec, "B": B, "K": K, "W": W, "mode": mode, "elapsed": elapsed, "kern_ms": kern_ms,
+           "ibar": ibar, "status_hist": status_hist, "solver": solver, "bnd": bnd, "ps_np": ps_np,
+           "pstep": pstep, "fov": timed_run.fov if mode == "fused" else None,
+           "chain": timed_run.chain, "info": timed_run.info if mode == "fused" else None,
+           "rows": getattr(fused, "rows", None), "side": None}
+    if per_step_side:
         e2, km2, ib2, h2 = timed_run("per_step", p0.clone(), w0.clone())
-        side = {"mode": "per_step (one solve launch + one shift launch per MPC step)",
-                "value": B * world * K / e2, "ms_per_step": e2 / K * 1e3,
-                "kernel_avg_ms": float(np.mean(km2)), "kernel_max_ms": float(np.max(km2)),
-                "mean_ip_iterations": ib2, "status_histogram": h2}
+        res["side"] = {"mode": "per_step (one solve launch + one shift launch per MPC step)",
+                       "value": B * world * K / e2, "ms_per_step": e2 / K * 1e3,
+                       "kernel_avg_ms": float(np.mean(km2)), "kernel_max_ms": float(np.max(km2)),
+                       "mean_ip_iterations": ib2, "status_histogram": h2}
+    return res
 
-    if rank == 0:
-        total_steps = B * world * K
-        value = total_steps / elapsed
-        ms_per_step = elapsed / K * 1e3
-        n_launch = len(kern_ms)
-        kern_avg_s = float(np.mean(kern_ms)) / 1e3
-        steps_per_launch = K if args.mode == "fused" else 1
-        kname = "nmpc_closed_loop_kernel" if args.mode == "fused" else "nmpc_solve_kernel"
-        if args.mode == "fused" and timed_run.info["policy"] == "step_queues":
-            kname = "nmpc_closed_loop_sched_kernel"
-        flops_launch = B * steps_per_launch * ibar * (spec.N + 1) * KFLOP_PER_STAGE_ITER * 1e3
-        achieved_tf = flops_launch / kern_avg_s / 1e12
-        bps, s_stage, b_iter, io = survey_bytes_per_step(spec, ibar)
-        achieved_gbs = B * steps_per_launch * bps / kern_avg_s / 1e9
-        pmc = pmc_summary(kname, K if args.mode == "fused" else None, B, W)
-        traffic = pmc["traffic"] if pmc else None
-        mode_txt = {"fused": f"{K} warm-started closed-loop MPC steps per scenario in one launch",
-                    "per_step": "warm-started closed-loop MPC steps, one launch per step",
-                    "cold": "cold-start (u=0) solves, one launch per step"}[args.mode]
-        res = {
-            "metric": METRIC,
-            "value": value, "unit": "MPC steps/s", "n_gpus": world, "steps": K,
-            "warmup": W, "ms_per_step": ms_per_step, "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
-            "config": {"workload": (f"config 4 family: {B * world} scenarios sharded {B}/GPU over {world} GPUs, "
-                                    if world > 1 and args.config == 3 else "")
-                                   + f"config {args.config}: batch={B}/GPU, "
-                                   f"{'no-gimbal 5-state' if spec.model == 'uav5' else '8-state UAV+gimbal'}, "
-                                   f"N={spec.N}, {spec.n_obs} obstacles"
-                                   + (" (moving per MATLAB/Dynamic Obstacles schedule)" if pstep is not None
-                                      else " static (Race Track 2.py layout)" if spec.n_obs else "")
-                                   + f", T={spec.T}, "
-                                   f"reference IPOPT opts, {mode_txt}",
-                       "global_batch": B * world, "seq_len": spec.N, "parallelism": f"dp{world}"},
-            "roofline": {"bound": "hbm", "achieved": achieved_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved_gbs / HBM_PEAK_GBS, "traffic": traffic,
-                         "traffic_unit": "bytes per launch between L2 and the fabric (Infinity Cache or HBM): "
-                                         "2*FETCH_SIZE + WRITE_SIZE, rocprofv3 PMC (calibrated x2 for 8 and 16 B/lane "
-                                         "reads, scripts/fetch_calib.hip)",
-                         "traffic_source": pmc["source"] if pmc else None,
-                         "counter_bytes_frac": (traffic / kern_avg_s / 1e9 / HBM_PEAK_GBS) if traffic else None,
-                         "pmc_runs": pmc["profiled_runs"] if pmc else None,
-                         "sq": pmc.get("sq") if pmc else None,
-                         "l2_hit_rate": pmc.get("l2_hit_rate") if pmc else None,
-                         "kernel": kname, "kernel_avg_ms": kern_avg_s * 1e3, "launches": n_launch,
-                         "model": f"SURVEY 8(d) streamed-KKT bytes: I_bar x B_iter + IO = {bps:.0f} B per "
-                                  f"MPC step (I_bar={ibar:.2f}, B_iter={b_iter} B, IO={io} B) x B={B} x "
-                                  f"{steps_per_launch} step(s) per launch / kernel time",
-                         "fp64": {"achieved_tflops": achieved_tf, "peak_tflops": FP64_PEAK_TFLOPS,
-                                  "frac": achieved_tf / FP64_PEAK_TFLOPS,
-                                  "model": f"{KFLOP_PER_STAGE_ITER} kflop/stage-iteration x (N+1) x I_bar"},
-                         "io_only_GBs": B * steps_per_launch * io / kern_avg_s / 1e9},
-            "mean_ip_iterations": ibar,
-            "status_histogram": status_hist,
-        }
-        if args.mode == "fused":
-            # the launch is bounded by its longest scenario chain (K steps of up to max_iter
-            # iterations each) and by the total work over the persistent slots
-            ch = timed_run.chain
-            slots = timed_run.info["launched_waves"] if timed_run.info["policy"] == "step_queues" else B
-            res["roofline"]["chain"] = {
-                "max_chain_iterations": int(ch.max()), "mean_chain_iterations": float(ch.mean()),
-                "total_iterations": int(ch.sum()), "slots": int(min(slots, B)),
-                "ms_per_chain_iteration": kern_avg_s * 1e3 / float(ch.max()),
-                "work_bound_iterations_per_slot": float(ch.sum()) / min(slots, B),
-                "note": "launch >= max(max_chain, total/slots) x per-iteration time"}
-        if args.mode == "fused":
-            info = timed_run.info
-            first = ("index order" if (args.in_order or W == 0) else
-                     "longest-expected-first by the iterations of the "
-                     f"{W} warm-up MPC steps that precede the timed steps (nmpc_amd.schedule)")
-            if info["policy"] == "step_queues":
-                res["dispatch"] = (f"step queues: {info['launched_waves']} persistent waves claim (scenario, step) "
-                                   f"pairs whose previous step is done, lowest step first, scenarios pinned to an "
-                                   f"XCD; initial order {first}")
-            else:
-                res["dispatch"] = f"one workgroup per scenario, {first}"
-            res["scheduler_error"] = info["scheduler_error"]
-            res["steps_done"] = info["steps_done"]
-        if fov_mean is not None:
-            res["closed_loop_fov_error_mean_m"] = fov_mean  # Python/NMPC_TT.py:433-437 metric, per step
-        if side is not None:
-            res["per_step_launch"] = side
-        if cpu_res is not None:
-            res["cpu_baseline"] = cpu_res
-            if world == 1 and getattr(cpu_baseline, "records", None):
-                res["parity_sample"] = parity_sample(solver, spec, cpu_baseline.start, K, cpu_baseline.records,
-                                                     bnd, dev, p_step=None if ps_np is None else ps_np[W:W + K])
-        print(json.dumps(res))
-        if args.dump_rows and args.mode == "fused":
-            np.save(args.dump_rows, fused.rows.cpu().numpy())
-    if world > 1:
-        dist.destroy_process_group()
+
+def result_line(args, m, world):
+    """The bench JSON fields of one measured configuration (BASELINE.json metric)."""
+    spec, B, K, W, mode = m["spec"], m["B"], m["K"], m["W"], m["mode"]
+    elapsed, kern_ms, ibar = m["elapsed"], m["kern_ms"], m["ibar"]
+    total_steps = B * world * K
+    value = total_steps / elapsed
+    ms_per_step = elapsed / K * 1e3
+    n_launch = len(kern_ms)
+    kern_avg_s = float(np.mean(kern_ms)) / 1e3
+    steps_per_launch = K if mode == "fused" else 1
+    kname = "nmpc_closed_loop_kernel" if mode == "fused" else "nmpc_solve_kernel"
+    if mode == "fused" and m["info"]["policy"] == "step_queues":
+        kname = "nmpc_closed_loop_sched_kernel"
+    flops_launch = B * steps_per_launch * ibar * (spec.N + 1) * KFLOP_PER_STAGE_ITER * 1e3
+    achieved_tf = flops_launch / kern_avg_s / 1e12
+    bps, s_stage, b_iter, io = survey_bytes_per_step(spec, ibar)
+    achieved_gbs = B * steps_per_launch * bps / kern_avg_s / 1e9
+    pmc = pmc_summary(kname, K if mode == "fused" else None, B, W)
+    traffic = pmc["traffic"] if pmc else None
+    mode_txt = {"fused": f"{K} warm-started closed-loop MPC steps per scenario in one launch",
+                "per_step": "warm-started closed-loop MPC steps, one launch per step",
+                "cold": "cold-start (u=0) solves, one launch per step"}[mode]
+    res = {
+        "metric": METRIC,
+        "value": value, "unit": "MPC steps/s", "n_gpus": world, "steps": K,
+        "warmup": W, "ms_per_step": ms_per_step, "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
+        "config": {"workload": (f"config 4 family: {B * world} scenarios sharded {B}/GPU over {world} GPUs, "
+                                if world > 1 and m["cfg"] == 3 else "")
+                               + f"config {m['cfg']}: batch={B}/GPU, "
+                               f"{'no-gimbal 5-state' if spec.model == 'uav5' else '8-state UAV+gimbal'}, "
+                               f"N={spec.N}, {spec.n_obs} obstacles"
+                               + (" (moving per MATLAB/Dynamic Obstacles schedule)" if m["pstep"] is not None
+                                  else " static (Race Track 2.py layout)" if spec.n_obs else "")
+                               + f", T={spec.T}, "
+                               f"reference IPOPT opts, {mode_txt}",
+                   "global_batch": B * world, "seq_len": spec.N, "parallelism": f"dp{world}"},
+        "roofline": {"bound": "hbm", "achieved": achieved_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved_gbs / HBM_PEAK_GBS, "traffic": traffic,
+                     "traffic_unit": "bytes per launch between L2 and the fabric (Infinity Cache or HBM): "
+                                     "2*FETCH_SIZE + WRITE_SIZE, rocprofv3 PMC (calibrated x2 for 8 and 16 B/lane "
+                                     "reads, scripts/fetch_calib.hip)",
+                     "traffic_source": pmc["source"] if pmc else None,
+                     "counter_bytes_frac": (traffic / kern_avg_s / 1e9 / HBM_PEAK_GBS) if traffic else None,
+                     "pmc_runs": pmc["profiled_runs"] if pmc else None,
+                     "sq": pmc.get("sq") if pmc else None,
+                     "l2_hit_rate": pmc.get("l2_hit_rate") if pmc else None,
+                     "kernel": kname, "kernel_avg_ms": kern_avg_s * 1e3, "launches": n_launch,
+                     "model": f"SURVEY 8(d) streamed-KKT bytes: I_bar x B_iter + IO = {bps:.0f} B per "
+                              f"MPC step (I_bar={ibar:.2f}, B_iter={b_iter} B, IO={io} B) x B={B} x "
+                              f"{steps_per_launch} step(s) per launch / kernel time",
+                     "fp64": {"achieved_tflops": achieved_tf, "peak_tflops": FP64_PEAK_TFLOPS,
+                              "frac": achieved_tf / FP64_PEAK_TFLOPS,
+                              "model": f"{KFLOP_PER_STAGE_ITER} kflop/stage-iteration x (N+1) x I_bar"},
+                     "io_only_GBs": B * steps_per_launch * io / kern_avg_s / 1e9},
+        "mean_ip_iterations": ibar,
+        "status_histogram": m["status_hist"],
+    }
+    if mode == "fused":
+        # the launch is bounded by its longest scenario chain (K steps of up to max_iter
+        # iterations each) and by the total work over the persistent slots
+        ch = m["chain"]
+        info = m["info"]
+        slots = info["launched_waves"] if info["policy"] == "step_queues" else B
+        res["roofline"]["chain"] = {
+            "max_chain_iterations": int(ch.max()), "mean_chain_iterations": float(ch.mean()),
+            "total_iterations": int(ch.sum()), "slots": int(min(slots, B)),
+            "ms_per_chain_iteration": kern_avg_s * 1e3 / float(ch.max()),
+            "work_bound_iterations_per_slot": float(ch.sum()) / min(slots, B),
+            "note": "launch >= max(max_chain, total/slots) x per-iteration time"}
+        first = ("index order" if (args.in_order or W == 0) else
+                 "longest-expected-first by the iterations of the "
+                 f"{W} warm-up MPC steps that precede the timed steps (nmpc_amd.schedule)")
+        if info["policy"] == "step_queues":
+            res["dispatch"] = (f"step queues: {info['launched_waves']} persistent waves claim (scenario, step) "
+                               f"pairs whose previous step is done, lowest step first, scenarios pinned to an "
+                               f"XCD; initial order {first}")
+        else:
+            res["dispatch"] = f"one workgroup per scenario, {first}"
+        res["scheduler_error"] = info["scheduler_error"]
+        res["steps_done"] = info["steps_done"]
+        if m["fov"] is not None:
+            res["closed_loop_fov_error_mean_m"] = m["fov"]  # Python/NMPC_TT.py:433-437 metric, per step
+    return res
 
 
 if __name__ == "__main__":

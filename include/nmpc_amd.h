@@ -140,8 +140,9 @@ int nmpc_dims(const nmpc_handle* h, int32_t* nw, int32_t* ng, int32_t* np, int32
  * rows with lbg == ubg are IPOPT's equality constraints c(x) = g(x) - lbg = 0 (no slack,
  * no relaxation; augmented-system step with IPOPT's inertia test), up to 128
  * per scenario.  A batch with any equality row runs on the equality class (global rows,
- * any shape): the host enqueues a bounds scan and both classes, and a device flag lets
- * exactly one of them run (no host round trip; the same for the _dev entry points).
+ * any shape, ~850 KB of device workspace per scenario): this host-pointer entry point scans
+ * the bounds on the host, allocates that workspace when the batch needs it and launches
+ * the one class that applies.
  * lbx > ubx, more than 128 equality rows, or equality rows with the fp32 Riccati leg
  * report status -11 (IPOPT Invalid_Problem_Definition) for that scenario. */
 int nmpc_solve_batch(nmpc_handle* h, int32_t B,
@@ -154,7 +155,13 @@ int nmpc_solve_batch(nmpc_handle* h, int32_t B,
                      int32_t* status, int32_t* iters);
 
 /* Same with DEVICE pointers, enqueued on `stream` (hipStream_t; NULL = default
- * stream); returns without synchronising.  Outputs other than x_out may be NULL. */
+ * stream); returns without synchronising (no host round trip: once the handle's workspace
+ * covers B, a call only enqueues kernels).  Outputs other than x_out may be NULL.
+ * Equality rows: the bounds are scanned on the device and a device flag lets exactly one
+ * of the problem's class and the equality class run.  The equality class needs its
+ * workspace reserved for B scenarios beforehand (nmpc_reserve_eq); without it a batch that
+ * has equality rows is not solved and every scenario reports NMPC_STATUS_EQ_UNRESERVED
+ * (x_out and f NaN).  Batches without equality rows need no reservation. */
 int nmpc_solve_batch_dev(nmpc_handle* h, int32_t B,
                          const double* x0, int64_t ld_x0,
                          const double* lbx, int64_t ld_lbx, const double* ubx, int64_t ld_ubx,
@@ -163,6 +170,16 @@ int nmpc_solve_batch_dev(nmpc_handle* h, int32_t B,
                          double* x_out, double* f_out, double* g_out,
                          double* lam_x_out, double* lam_g_out, double* lam_p_out, double* X_out,
                          int32_t* status, int32_t* iters, void* stream);
+
+/* Per-scenario status of a device-pointer call (nmpc_solve_batch_dev, nmpc_closed_loop_dev)
+ * whose batch has equality rows (lbg == ubg) while the equality class's workspace does not
+ * cover B: the batch was not solved (IPOPT's Insufficient_Memory code).  Reserve first. */
+#define NMPC_STATUS_EQ_UNRESERVED (-102)
+/* Allocate the equality class's device workspace for B scenarios (synchronous, like any
+ * allocation; a no-op when it already covers B or for the fp32 leg, whose equality rows
+ * report -11).  The _dev entry points never allocate it themselves, so that they never
+ * synchronise the host; nmpc_solve_batch allocates it on demand. */
+int nmpc_reserve_eq(nmpc_handle* h, int32_t B);
 
 /* Optional per-iteration trace (debugging / parity): when enabled, the next
  * solve records NMPC_TRACE_FIELDS doubles per iteration per scenario into a
@@ -241,7 +258,9 @@ int nmpc_closed_loop_dev(nmpc_handle* h, int32_t B, int32_t K,
  *     the first launch).  waves: workgroups the last launch started.
  *   sched_err: bit 0 a wave gave up waiting for a published step, bit 1 a scenario did
  *     not complete its K steps (its unrun steps carry status and iterations
- *     NMPC_STATUS_NOT_RUN and NaN f / fov / u / x in the histories).  0 on success.
+ *     NMPC_STATUS_NOT_RUN and NaN f / fov / u / x in the histories), bit 2 the batch has
+ *     equality rows and the equality workspace was not reserved (nmpc_reserve_eq): no step
+ *     ran, and they carry NMPC_STATUS_EQ_UNRESERVED instead.  0 on success.
  *   steps_done: closed-loop steps completed, counted per scenario by a check kernel
  *     after either policy's launch (must equal B*K; 64-bit). */
 #define NMPC_STATUS_NOT_RUN (-1000)
@@ -265,9 +284,9 @@ const char* nmpc_build_id(void);
 int nmpc_kernel_info(const nmpc_handle* h, int32_t* lds_bytes, int32_t* threads_per_scenario);
 
 /* Device workspace the handle holds (bytes): the problem class's per-scenario
- * workspace, and the equality class's, which is allocated only once a
- * batch with equality rows (lbg == ubg) has been solved and is 0 until then; per
- * scenario: the class layouts' sizes (ws_per_scenario, wsE_per_scenario; nullable). */
+ * workspace, and the equality class's, which is allocated only by
+ * nmpc_reserve_eq or by a host-pointer batch with equality rows (lbg == ubg) and is 0 until
+ * then; per scenario: the class layouts' sizes (ws_per_scenario, wsE_per_scenario; nullable). */
 int nmpc_memory_info(const nmpc_handle* h, int64_t* ws_bytes, int64_t* ws_eq_bytes, int64_t* ws_per_scenario,
                      int64_t* wsE_per_scenario);
 

@@ -68,6 +68,8 @@ struct Params {
   double ox[NMPC_MAX_OBS], oy[NMPC_MAX_OBS], orr[NMPC_MAX_OBS];
   int oxp[NMPC_MAX_OBS], oyp[NMPC_MAX_OBS];
   nmpc_options o;
+  int nospec;  // diagnostics (NMPC_NO_SPEC=1 at nmpc_create): no speculative restoration trial pairs
+  double thv, thh;  // tan(hv), tan(hh) (host libm): the FOV tangent pairs from one tangent (NMPC_TAN2)
 };
 
 // Per-scenario memory layout (offsets in doubles).  Computed at compile time
@@ -262,6 +264,40 @@ __device__ __forceinline__ double wreduce(double v, OP op) {
 __device__ __forceinline__ double wsum(double v) {
   return wreduce(v, [](double a, double b) { return a + b; });
 }
+// Sum of logarithms as the logarithm of a product (the barrier terms mu * sum log(slack)
+// of IPOPT's phi): a lane keeps the product of its arguments as a mantissa in [0.5, 1)
+// (v_frexp_mant) and a binary exponent (v_frexp_exp), renormalised after every factor so
+// it can neither overflow nor underflow, and takes ONE logarithm at the end:
+//   sum log(x_i) = log(m) + e ln 2,  ln 2 split so that e * LN2_HI is exact.
+// A factor costs a multiply and two frexp instead of an fp64 log (~90 dependent
+// operations, the row passes' largest cost).  The result differs from the sum of the
+// logarithms at the rounding level only: the product carries <= n ulp of relative error
+// (n factors per lane, <= 24), i.e. <= 3e-15 absolute in the lane's log sum, below the
+// rounding of the sum it replaces.  A non-positive argument gives log(<= 0) = NaN / -inf
+// as the sum did, so a trial outside the bounds is still rejected as non-finite.
+struct LogAcc {
+  double m = 1.0;
+  int e = 0;
+  __device__ __forceinline__ void mul(double x) {
+    const double p = m * x;
+    m = __builtin_amdgcn_frexp_mant(p);
+    e += __builtin_amdgcn_frexp_exp(p);
+  }
+  // two factors: their product first (|x|, |y| < 2^500: no overflow), one renormalisation
+  __device__ __forceinline__ void mul2(double x, double y) {
+    const double xy = x * y;
+    const double xe = __builtin_amdgcn_frexp_mant(xy);
+    const int ee = __builtin_amdgcn_frexp_exp(xy);
+    const double p = m * xe;
+    m = __builtin_amdgcn_frexp_mant(p);
+    e += ee + __builtin_amdgcn_frexp_exp(p);
+  }
+  __device__ __forceinline__ double log() const {
+    constexpr double LN2_HI = 6.93147180369123816490e-01, LN2_LO = 1.90821492927058770002e-10;
+    const double de = (double)e;
+    return (::log(m) + de * LN2_LO) + de * LN2_HI;
+  }
+};
 __device__ __forceinline__ double wmax(double v) {
   return wreduce(v, [](double a, double b) { return fmax(a, b); });
 }
@@ -633,6 +669,27 @@ struct Solver {
     sync();
   }
 
+  // The FOV tangents tan(x +- h) of one angle (NMPC_TT.py:209-214).  NMPC_TAN2: from the
+  // one tangent t = tan(x) by the addition formula, tan(x +- h) = (t +- tan h) / (1 -+ t tan h)
+  // with tan h formed on the host -- one fp64 tangent (OCML: a Payne-Hanek / Cody-Waite
+  // reduction and a rational approximation, ~100 dependent operations) and two reciprocals
+  // instead of two tangents; a few ulp apart from the direct forms (no cancellation in
+  // 1 -+ t tan h while |x| < pi/2 - h).
+#ifndef NMPC_TAN2
+#define NMPC_TAN2 0
+#endif
+  __device__ __forceinline__ static void tan_pm(double x, double h, double th, double& tp, double& tm) {
+    if constexpr (NMPC_TAN2) {
+      const double t = tan(x);
+      const double ct = t * th;
+      tp = (t + th) * rcp(1.0 - ct);
+      tm = (t - th) * rcp(1.0 + ct);
+    } else {
+      tp = tan(x + h);
+      tm = tan(x - h);
+    }
+  }
+
   // ---------------------------------------------------------- stage cost value
   // Literal restatement of NMPC_TT.py:209-220 (same operation order as the
   // oracle's stage_cost).
@@ -640,7 +697,9 @@ struct Solver {
   __device__ __forceinline__ double stage_cost(const LDS double* x, GLB double* tw = nullptr) const {
     const double hv = P->hv, hh = P->hh;
     const double z = x[2];
-    const double t6p = tan(x[6] + hv), t6m = tan(x[6] - hv), t5p = tan(x[5] + hh), t5m = tan(x[5] - hh);
+    double t6p, t6m, t5p, t5m;
+    tan_pm(x[6], hv, P->thv, t6p, t6m);
+    tan_pm(x[5], hh, P->thh, t5p, t5m);
     const double a = (z * t6p - z * t6m) / 2;
     const double bb = (z * t5p - z * t5m) / 2;
     const double c7 = cos(x[7]), s7 = sin(x[7]);
@@ -727,6 +786,17 @@ struct Solver {
   // sits in lanes 32..63 -- the butterfly reduces each 32-lane half in the same order, so
   // both objectives are bitwise those of two separate calls.
   static constexpr bool kSpec = CAP::lds_rows && !CAP::refine && !CAP::eq && CAP::nmax <= 31;
+  // Scratch of a pair's second trial: its increments in qs (stride 8, rows 0..nmax + 1, so
+  // they overwrite the S_k terms qs[k*10 + 8..9]), its X in lam, its rows in dms.  This is
+  // sound because (i) every Newton assembly rewrites qs[k*10 + 8..9] before the next
+  // factorisation reads them, and nothing else reads them between (the restoration SOC
+  // block's assemble(SUM_RESTO_SOC) writes q_k only, resolve / forward read q_k only, and
+  // the refinement that reads S_k is compiled out of the kSpec classes); (ii) between the
+  // pair's formation and a from_pair acceptance nothing writes lam or dms (the SOC block's
+  // re-solve, forward sweep, row step and spec = 0 trial write qs[0..7], dX, ds2, the
+  // *2R vectors, Xt and dt).  Bitwise check against Params::nospec:
+  // test_speculative_restoration_pairs_are_bitwise_neutral.
+  static_assert(!kSpec || 8 * (CAP::nmax + 2) <= 10 * (CAP::nmax + 1), "qs cannot hold a pair's increments");
   __device__ __forceinline__ void rollout2(const GLB double* Us, const GLB double* dUs, double a0, double a1,
                                            const UPre* pre = nullptr) {
     STAMP0();
@@ -856,8 +926,13 @@ struct Solver {
         const double hv = P->hv, hh = P->hh;
         const double x = xk[0], yy = xk[1], z = xk[2], x5 = xk[5], x6 = xk[6], x7 = xk[7];
         const double xt = pp[8], yt = pp[9];
-        const double t6p = TC ? tk[4] : tan(x6 + hv), t6m = TC ? tk[5] : tan(x6 - hv);
-        const double t5p = TC ? tk[6] : tan(x5 + hh), t5m = TC ? tk[7] : tan(x5 - hh);
+        double t6p, t6m, t5p, t5m;
+        if constexpr (TC) {
+          t6p = tk[4]; t6m = tk[5]; t5p = tk[6]; t5m = tk[7];
+        } else {
+          tan_pm(x6, hv, P->thv, t6p, t6m);
+          tan_pm(x5, hh, P->thh, t5p, t5m);
+        }
         const double al6 = (t6p - t6m) / 2, be6 = (t6p + t6m) / 2;
         const double al5 = (t5p - t5m) / 2, be5 = (t5p + t5m) / 2;
         const double al6d = (t6p * t6p - t6m * t6m) / 2, be6d = (2 + t6p * t6p + t6m * t6m) / 2;
@@ -1102,35 +1177,32 @@ struct Solver {
   // the sums are kept in rvars[32..33], so the accepted trial's sums serve the next
   // iteration's reference value (same slacks bit for bit: U <- Ut, s <- s + a ds)
   // per-lane partial sums: the control terms first, then the rows in rows() order
-  __device__ __forceinline__ void barrier_ctrl(const GLB double* u, double& logs, double& damp) const {
+  // (the log sums as LogAcc products, one logarithm per lane and pass)
+  __device__ __forceinline__ void barrier_ctrl(const GLB double* u, LogAcc& logs, double& damp) const {
     ctrls([&](int i, bool on) { barrier_ctrl1(i, on, u[i], logs, damp); });
   }
   // one control's barrier terms at the value ui (a register: the trial point's controls
   // are formed and consumed in the same pass, no store -> load round trip)
-  __device__ __forceinline__ void barrier_ctrl1(int i, bool on, double ui, double& logs, double& damp) const {
+  __device__ __forceinline__ void barrier_ctrl1(int i, bool on, double ui, LogAcc& logs, double& damp) const {
     const double xli = xl[i], xui = xu[i];
     const bool lo = hasl(xli), hi = hasu(xui);
-    const double ll = log(ui - xli), lu = log(xui - ui);
+    logs.mul2(on && lo ? ui - xli : 1.0, on && hi ? xui - ui : 1.0);
     if (on) {
-      if (lo) logs += ll;
-      if (hi) logs += lu;
       if (lo && !hi) damp += ui - xli;
       if (hi && !lo) damp += xui - ui;
     }
   }
-  __device__ __forceinline__ void barrier_row(int r, bool on, double sv, double& logs, double& damp) const {
+  __device__ __forceinline__ void barrier_row(int r, bool on, double sv, LogAcc& logs, double& damp) const {
     const double lo_ = dl[r], hi_ = du[r];
     const bool lo = hasl(lo_), hi = hasu(hi_);
-    const double ll = log(sv - lo_), lu = log(hi_ - sv);  // both logs of a row pair in flight
+    logs.mul2(on && lo ? sv - lo_ : 1.0, on && hi ? hi_ - sv : 1.0);
     if (on) {
-      if (lo) logs += ll;
-      if (hi) logs += lu;
       if (lo && !hi) damp += sv - lo_;
       if (hi && !lo) damp += hi_ - sv;
     }
   }
-  __device__ __forceinline__ double barrier_fin(double f, double logs, double damp) {
-    logs = wsum(logs);
+  __device__ __forceinline__ double barrier_fin(double f, const LogAcc& la, double damp) {
+    const double logs = wsum(la.log());
     damp = wsum(damp);
     rvars[32] = logs; rvars[33] = damp;
     return phi_of(f, logs, damp);
@@ -1138,7 +1210,8 @@ struct Solver {
   __device__ __forceinline__ double barrier_obj(double f, const GLB double* u, const RV* sb, const RV* dsv,
                                 double a) {
     STAMP0();
-    double logs = 0.0, damp = 0.0;
+    LogAcc logs;
+    double damp = 0.0;
     barrier_ctrl(u, logs, damp);
     rows([&](int r, bool on) { barrier_row(r, on, dsv ? sb[r] + a * dsv[r] : sb[r], logs, damp); });
     const double rr = barrier_fin(f, logs, damp);
@@ -1711,6 +1784,8 @@ struct Solver {
     // next trial before any read), in the classes that keep dt in LDS; K column ln (lanes
     // 0..7) and R~ entry tR are stored through per-lane base pointers
     constexpr bool kDummy = CAP::lds_rows && !CAP::refine;
+    // the dead-slot stores reach dt[191] (dmy + 128 + lane): dt must hold 192 doubles
+    static_assert(!kDummy || al2(CAP::mmax * (CAP::nmax + 1)) >= 192, "dt too small for the branch-free Riccati stores");
     LDS R* dmy = kDummy ? (LDS R*)dt : Stc;
     LDS R* const st_dst = ln < 48 ? Stc + ln : dmy + ln;
     LDS R* const rc_dst = tR0 >= 0 ? Rcc + tR : dmy + 64 + ln;
@@ -2407,20 +2482,19 @@ struct Solver {
   }
   __device__ __forceinline__ double resto_pn_terms(const GLB double* Us, double a, const GLB double* dps,
                                                    const GLB double* dns) {
-    double pn = 0.0, lg = 0.0, prox = 0.0;
+    double pn = 0.0, prox = 0.0;
+    LogAcc la;
     rows_r([&](int r, bool on) {
       const double pv = dps ? pR[r] + a * dps[r] : pR[r], nv = dns ? nR[r] + a * dns[r] : nR[r];
-      const double l2 = log(pv) + log(nv);
-      if (on) {
-        pn += pv + nv;
-        lg += l2;
-      }
+      la.mul2(on ? pv : 1.0, on ? nv : 1.0);
+      if (on) pn += pv + nv;
     });
     for (int i = lanef(); i < nw; i += WAVE) {
       const double dd = Us[i] - UR[i];
       prox += dr2(i) * dd * dd;
     }
-    pn = wsum(pn); lg = wsum(lg); prox = wsum(prox);
+    double lg;
+    pn = wsum(pn); lg = wsum(la.log()); prox = wsum(prox);
     rvars[34] = pn; rvars[35] = lg; rvars[36] = prox;
     return pn_of(pn, lg, prox);
   }
@@ -2440,7 +2514,8 @@ struct Solver {
     XSTAMP0(_x0);
     UPre up;  // (a pair's second trial forms no rollout)
     if (spec != 2) up = preload_u(U, dUs, (kSpec && spec == 1) ? 31 : WAVE - 1);
-    double th = 0.0, logs = 0.0, damp = 0.0, pn = 0.0, lg = 0.0, prox = 0.0;
+    double th = 0.0, damp = 0.0, pn = 0.0, prox = 0.0;
+    LogAcc logs, la;  // the barrier terms' and the p / n terms' log sums
     ctrls([&](int i, bool on) {
       const double ui = U[i] + a * dUs[i];
       if (on) Ut[i] = ui;
@@ -2458,12 +2533,11 @@ struct Solver {
         const double sv = s[r] + a * dss[r], pv = pR[r] + a * dps[r], nv = nR[r] + a * dns[r];
         const double dtr = dtv[r];
         barrier_row(r, on, sv, logs, damp);
-        const double l2 = log(pv) + log(nv);
+        la.mul2(on ? pv : 1.0, on ? nv : 1.0);
         if (on) {
           th += fabs(dtr - sv - pv + nv);
           if (!isfinite(dtr)) bad = true;
           pn += pv + nv;
-          lg += l2;
         }
       });
     };
@@ -2506,7 +2580,8 @@ struct Solver {
     tht = wsum(th);
     if (wany(bad)) return false;
     const double phb = barrier_fin(0.0, logs, damp);
-    pn = wsum(pn); lg = wsum(lg); prox = wsum(prox);
+    double lg;
+    pn = wsum(pn); lg = wsum(la.log()); prox = wsum(prox);
     rvars[34] = pn; rvars[35] = lg; rvars[36] = prox;
     phit = phb + pn_of(pn, lg, prox);
     XSTAMP1(_x4, X_TFIN);
@@ -2696,7 +2771,8 @@ struct Solver {
                         double& tht) {
     // the trial controls and their barrier terms in one pass
     const UPre up = preload_u(U, dUs, WAVE - 1);
-    double th = 0.0, logs = 0.0, damp = 0.0;
+    double th = 0.0, damp = 0.0;
+    LogAcc logs;
     ctrls([&](int i, bool on) {
       const double ui = U[i] + a * dUs[i];
       if (on) Ut[i] = ui;
@@ -3179,6 +3255,9 @@ __device__ __forceinline__ void resto_phase(const Params* __restrict__ prm, doub
         // speculative pairs (Solver::kSpec): each trial not formed yet is formed together
         // with the next backtracking trial (spec_a), whose X / rows wait in lam / dms
         double spec_a = -1.0, spec_f = 0.0;
+        // (Params::nospec, a diagnostic: every trial formed alone -- the reference run of the
+        // bitwise test of the pairs, test_speculative_restoration_pairs_are_bitwise_neutral)
+        const bool spec_on = Solver<CAP>::kSpec && !prm->nospec;
         while (a > amin || nsteps == 0) {
           double fo_t, ph, th;
           bool ok_t;
@@ -3188,8 +3267,8 @@ __device__ __forceinline__ void resto_phase(const Params* __restrict__ prm, doub
             spec_a = -1.0;
           } else {
             const double an = a * o.alpha_red_factor;
-            ok_t = S.trial_resto(a, S.dU, S.ds, S.dpR, S.dnR, fo_t, ph, th, Solver<CAP>::kSpec ? 1 : 0, an, &spec_f);
-            spec_a = Solver<CAP>::kSpec ? an : -1.0;
+            ok_t = S.trial_resto(a, S.dU, S.ds, S.dpR, S.dnR, fo_t, ph, th, spec_on ? 1 : 0, an, &spec_f);
+            spec_a = spec_on ? an : -1.0;
           }
           if (ok_t && r_check(a, ph, th)) {
             acc = 1; V[19] = a; V[20] = fo_t; V[21] = ph; a_test = a;
@@ -4601,6 +4680,7 @@ struct SchedQ {
   int one_set;  // test hook (NMPC_SCHED_TEST_ONE_SET): only the waves on XCD 0 run, so
                 // sets 1..7 are never drained and the check must report it
   int hot_iters;  // a step after one with >= hot_iters iterations goes to the hot family (0: none)
+  const int* eqnows;  // the equality gate flag when the equality class was not launched (nullable)
 };
 constexpr unsigned long long kSchedWaitTicks = 1000000000ull;  // s_memrealtime (100 MHz): 10 s
 
@@ -4752,6 +4832,22 @@ __global__ void nmpc_eq_scan_kernel(long long n, int ng, const double* lbg, long
   if (eq) *flag = 1;
 }
 
+// a device-pointer solve whose batch has equality rows while the equality class's
+// workspace is not reserved (nmpc_reserve_eq): neither class of the pair ran, so every
+// scenario reports NMPC_STATUS_EQ_UNRESERVED (IPOPT Insufficient_Memory) with a NaN
+// objective and solution (no-op when the flag is 0: the problem's class ran)
+__global__ void nmpc_eq_unreserved_kernel(int B, const int* flag, int nw, double* x_out, double* f_out,
+                                          int* status, int* iters) {
+  if (*flag == 0) return;
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  const double nan = __builtin_nan("");
+  if (status) status[b] = NMPC_STATUS_EQ_UNRESERVED;
+  if (iters) iters[b] = 0;
+  if (f_out) f_out[b] = nan;
+  for (int i = 0; i < nw; ++i) x_out[(long long)b * nw + i] = nan;
+}
+
 // completion-guard state of a one-workgroup-per-scenario launch (no queues)
 __global__ void nmpc_guard_init_kernel(int B, SchedQ q) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -4764,18 +4860,23 @@ __global__ void nmpc_guard_init_kernel(int B, SchedQ q) {
 // A scenario that did not sets err[0] |= 2, and its unrun steps are marked in every
 // history (status / iterations NMPC_STATUS_NOT_RUN; f, fov, u, x NaN) so nothing is
 // left uninitialised.
+// A batch with equality rows whose equality class was not launched (its workspace not
+// reserved, nmpc_reserve_eq; q.eqnows = the gate flag) ran no step: err |= 4 as well, and
+// the steps carry NMPC_STATUS_EQ_UNRESERVED instead of NMPC_STATUS_NOT_RUN.
 __global__ void nmpc_sched_check_kernel(int B, int K, SchedQ q, const Loop lp) {
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= B) return;
   const int d = q.done[b];
   atomicAdd(q.ndone, (unsigned long long)(d < 0 ? 0 : d));
   if (d == K) return;
-  atomicOr(q.err, 2);
+  const bool nows = q.eqnows && *q.eqnows != 0;
+  atomicOr(q.err, nows ? 6 : 2);
+  const int code = nows ? NMPC_STATUS_EQ_UNRESERVED : NMPC_STATUS_NOT_RUN;
   const double nan = __builtin_nan("");
   for (int k = d < 0 ? 0 : d; k < K; ++k) {
     const long long kb = (long long)k * B + b;
-    if (lp.st_hist) lp.st_hist[kb] = NMPC_STATUS_NOT_RUN;
-    if (lp.it_hist) lp.it_hist[kb] = NMPC_STATUS_NOT_RUN;
+    if (lp.st_hist) lp.st_hist[kb] = code;
+    if (lp.it_hist) lp.it_hist[kb] = code;
     if (lp.f_hist) lp.f_hist[kb] = nan;
     if (lp.fov_hist) lp.fov_hist[kb] = nan;
     if (lp.u_hist)
@@ -4974,35 +5075,32 @@ static int ensure_ws(nmpc_handle* h, int B) {
   return ensure_buf(&h->dws, &h->ws_bytes, (size_t)B * h->ws_doubles * sizeof(double), "workspace");
 }
 
-// Which kernels of the class pair a launch runs.  The equality class's workspace is
-// allocated lazily: while it does not cover B, the batch's bounds are scanned on the
-// device and the flag read back (one stream synchronisation), and only the class that
-// applies is launched -- the problem's own class when the batch has no equality row (its
-// workspace alone), the equality class (workspace allocated now) when it has.  Once that
-// workspace exists the pair is enqueued behind the device flag with no host round trip.
-// host_eq: -1 unknown (device pointers), 0 / 1 the host-side scan's answer.
-struct Run { bool A, E; };
+// Which kernels of the class pair a launch runs.  The equality class's workspace (~850 KB
+// per scenario) is allocated only when needed:
+//  * host pointers (nmpc_solve_batch, host_eq 0 / 1): the host has scanned the bounds, so
+//    exactly the class that applies is launched, and an equality batch allocates the
+//    equality workspace first;
+//  * device pointers (the _dev entry points, host_eq -1): never a host round trip.  The
+//    bounds are scanned on the device and the pair is enqueued behind the device flag.  If
+//    the equality workspace does not cover B (nmpc_reserve_eq was not called for this B),
+//    the equality class is not launched; a batch that has equality rows then reports
+//    NMPC_STATUS_EQ_UNRESERVED per scenario instead of running (run->Enows: the solve's
+//    marker kernel / the closed loop's completion check write it).
+struct Run { bool A, E, Enows; };
 static int eq_prepare(nmpc_handle* h, int B, IO& io, IO& ioE, hipStream_t st, int host_eq, Run* run) {
   ioE = io;
   io.eqflag = nullptr; ioE.eqflag = nullptr;
-  run->A = true; run->E = false;
+  run->A = true; run->E = false; run->Enows = false;
   if (!h->kernE) return NMPC_OK;  // fp32 leg, or NMPC_FORCE_CLASS=E: one class, no partner
   const size_t needE = (size_t)B * h->ws_doublesE * sizeof(double);
-  int eq = host_eq;
-  if (eq < 0 && needE > h->wsE_bytes) {
+  if (host_eq >= 0) {  // known: launch the one class that applies
+    run->A = host_eq == 0; run->E = host_eq == 1;
+  } else {  // the gated pair, decided on the device
     if (int rc = eq_gate(h, B, io, st)) return rc;
-    int flag = 0;
-    if (hipMemcpyAsync(&flag, h->deq, sizeof(int), hipMemcpyDeviceToHost, st) != hipSuccess ||
-        hipStreamSynchronize(st) != hipSuccess)
-      return fail(NMPC_E_HIP, "reading the equality-row flag");
-    eq = flag != 0;
-  }
-  if (eq >= 0) {  // known: launch the one class that applies
-    run->A = eq == 0; run->E = eq == 1;
-  } else {  // equality workspace in place: the gated pair, decided on the device
-    if (int rc = eq_gate(h, B, io, st)) return rc;
-    run->A = run->E = true;
     io.eqflag = h->deq; ioE.eqflag = h->deq;
+    run->A = true;
+    run->E = needE <= h->wsE_bytes;
+    run->Enows = !run->E;
   }
   if (run->E) {
     if (int rc = ensure_buf(&h->dwsE, &h->wsE_bytes, needE, "equality-class workspace")) return rc;
@@ -5099,6 +5197,7 @@ int nmpc_create(const nmpc_desc* desc, nmpc_handle** out) {
   P.nw = 6 * P.N; P.nwE = P.nuE * P.N; P.ng = P.m * (P.N + 1); P.nX = 8 * (P.N + 1);
   // the no-gimbal cost is the distance term alone (MATLAB/Dynamic Obstacles/NMPC_TT.m:102-105)
   P.T = desc->T; P.w1 = desc->w1; P.w2 = nog ? 0.0 : desc->w2; P.hv = desc->vfov / 2; P.hh = desc->hfov / 2;
+  P.thv = std::tan(P.hv); P.thh = std::tan(P.hh);
   P.w1p = pin(desc->w1_pidx); P.w2p = nog ? -1 : pin(desc->w2_pidx);
   for (int j = 0; j < NMPC_MAX_OBS; ++j) {
     P.oxp[j] = -1; P.oyp[j] = -1;
@@ -5108,6 +5207,7 @@ int nmpc_create(const nmpc_desc* desc, nmpc_handle** out) {
     P.oxp[j] = pin(desc->obs_x_pidx[j]); P.oyp[j] = pin(desc->obs_y_pidx[j]);
   }
   P.o = desc->opts;
+  if (const char* e = std::getenv("NMPC_NO_SPEC")) P.nospec = std::atoi(e) != 0;
   {
     int ldsd = 0;
     const bool forcedE = pick_class(P, &h->kern, &h->loop, &h->sched, &ldsd, &h->ws_doubles);
@@ -5219,6 +5319,14 @@ int nmpc_memory_info(const nmpc_handle* h, int64_t* ws_bytes, int64_t* ws_eq_byt
   return NMPC_OK;
 }
 
+int nmpc_reserve_eq(nmpc_handle* h, int32_t B) {
+  if (!h) return fail(NMPC_E_INVALID, "null handle");
+  if (B < 0) return fail(NMPC_E_INVALID, "B < 0");
+  if (!h->kernE || B == 0) return NMPC_OK;  // fp32 leg: equality rows report -11 anyway
+  return ensure_buf(&h->dwsE, &h->wsE_bytes, (size_t)B * h->ws_doublesE * sizeof(double),
+                    "equality-class workspace");
+}
+
 int nmpc_set_trace(nmpc_handle* h, int32_t enable) {
   if (!h) return fail(NMPC_E_INVALID, "null handle");
   h->trace = enable != 0;
@@ -5277,6 +5385,9 @@ static int solve_dev(nmpc_handle* h, int32_t B, const double* x0, int64_t ld_x0,
   if (run.E)
     hipLaunchKernelGGL(h->kernE, dim3(B), dim3(WAVE), h->lds_bytesE, (hipStream_t)stream,
                        (const Params*)h->dprm, (int)B, ioE);
+  if (run.Enows)
+    hipLaunchKernelGGL(nmpc_eq_unreserved_kernel, dim3((B + 255) / 256), dim3(256), 0, (hipStream_t)stream, (int)B,
+                       (const int*)h->deq, P.nwE, x_out, f_out, status, iters);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return fail(NMPC_E_HIP, std::string("kernel launch: ") + hipGetErrorString(e));
   return NMPC_OK;
@@ -5469,6 +5580,7 @@ int nmpc_closed_loop_dev(nmpc_handle* h, int32_t B, int32_t K, const double* lbx
   q.ndone = (unsigned long long*)h->dsched;
   q.err = h->dsched + 2;
   q.done = h->dsched + 4;
+  q.eqnows = run.Enows ? h->deq : nullptr;
   const int thr = 256;
   h->last_err = q.err;
   h->last_ndone = q.ndone;

@@ -12,6 +12,7 @@ import os
 MAX_OBS = 16
 MAX_N = 63
 TRACE_FIELDS = 12
+EQ_UNRESERVED = -102  # NMPC_STATUS_EQ_UNRESERVED (IPOPT Insufficient_Memory)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libnmpc_amd.so")
@@ -24,7 +25,7 @@ EXPORTS = (
     "nmpc_default_options", "nmpc_create", "nmpc_destroy", "nmpc_dims",
     "nmpc_solve_batch", "nmpc_solve_batch_dev", "nmpc_set_trace", "nmpc_read_trace",
     "nmpc_shift_dev", "nmpc_closed_loop_dev", "nmpc_closed_loop_info", "nmpc_last_error", "nmpc_kernel_info",
-    "nmpc_build_id", "nmpc_closed_loop_times", "nmpc_memory_info",
+    "nmpc_build_id", "nmpc_closed_loop_times", "nmpc_memory_info", "nmpc_reserve_eq",
 )
 
 _OPT_INT = ("max_iter", "acceptable_iter", "max_soc", "max_soft_resto_iters",
@@ -106,9 +107,11 @@ def lib():
     L.nmpc_build_id.restype = C.c_char_p
     L.nmpc_kernel_info.argtypes = [vp, i32p, i32p]
     L.nmpc_memory_info.argtypes = [vp] + [C.POINTER(C.c_int64)] * 4
+    if hasattr(L, "nmpc_reserve_eq") or not os.environ.get("NMPC_LIB"):  # (an older diagnostic build may lack it)
+        L.nmpc_reserve_eq.argtypes = [vp, C.c_int32]
     L.nmpc_closed_loop_info.argtypes = [vp, i32p, i32p, i32p, i32p, C.POINTER(C.c_int64)]
     for n in EXPORTS:
-        if n not in ("nmpc_default_options", "nmpc_last_error", "nmpc_build_id"):
+        if n not in ("nmpc_default_options", "nmpc_last_error", "nmpc_build_id") and hasattr(L, n):
             getattr(L, n).restype = C.c_int
     _lib = L
     return L

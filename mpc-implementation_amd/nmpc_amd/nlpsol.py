@@ -34,6 +34,7 @@ RETURN_STATUS = {
     3: "Search_Direction_Becomes_Too_Small", 4: "Diverging_Iterates",
     -1: "Maximum_Iterations_Exceeded", -2: "Restoration_Failed", -3: "Error_In_Step_Computation",
     -11: "Invalid_Problem_Definition", -13: "Invalid_Number_Detected",
+    -102: "Insufficient_Memory",  # NMPC_STATUS_EQ_UNRESERVED: equality rows, no reserve_equality(B)
 }
 _SUCCESS = (0, 1)
 NOT_RUN = -1000  # NMPC_STATUS_NOT_RUN: a closed-loop step the scheduler never ran
@@ -200,7 +201,10 @@ class Solver:
 
         ``out`` holds preallocated device tensors x (B,nw) [required], f (B,),
         g (B,ng), lam_x (B,nw), lam_g (B,ng), lam_p (B,np), X (B,nX), status/iters (B,) int32
-        (optional).  Enqueued on ``stream`` (torch stream; default = current).
+        (optional).  Enqueued on ``stream`` (torch stream; default = current); never
+        synchronises the host.  Batches with equality rows (lbg == ubg) need
+        ``reserve_equality(B)`` first, otherwise every scenario reports status -102
+        (Insufficient_Memory) with NaN x and f.
         """
         import torch  # plumbing only: device memory and streams
 
@@ -328,6 +332,13 @@ class Solver:
         if check:
             self.check_closed_loop(B, K)
 
+    def reserve_equality(self, B: int):
+        """Allocate the equality class's device workspace for B scenarios (nmpc_reserve_eq):
+        the device entry points (solve_device, closed_loop_device) never allocate it
+        themselves, so that they never synchronise the host.  The host-array call
+        (``solver(...)``) allocates it on demand."""
+        _lib.check(_lib.lib().nmpc_reserve_eq(self._h, int(B)))
+
     def set_trace(self, enable: bool):
         _lib.check(_lib.lib().nmpc_set_trace(self._h, int(enable)))
 
@@ -348,6 +359,10 @@ class Solver:
     def check_closed_loop(self, B: int, K: int):
         """Raise if the last closed-loop launch did not run every (scenario, step)."""
         info = self.closed_loop_info()
+        if info["scheduler_error"] & 4:
+            raise _lib.NmpcError("closed loop not run: the batch has equality rows (lbg == ubg) and the "
+                                 "equality workspace is not reserved (Solver.reserve_equality(B)); the steps "
+                                 f"carry status {_lib.EQ_UNRESERVED}")
         if info["scheduler_error"] != 0 or info["steps_done"] != B * K:
             raise _lib.NmpcError(f"closed loop incomplete: {info['steps_done']} of {B * K} steps run, "
                                  f"scheduler_error={info['scheduler_error']} (unrun steps carry status "

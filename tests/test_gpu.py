@@ -261,6 +261,118 @@ def test_device_path_matches_host_path():
     np.testing.assert_array_equal(out["status"].cpu().numpy(), s.stats()["status_code"])
 
 
+def test_dev_entry_points_do_not_synchronise():
+    """nmpc_solve_batch_dev and nmpc_closed_loop_dev only enqueue work (include/nmpc_amd.h:
+    "returns without synchronising").  Enqueued on a side stream behind a kernel that spins for
+    ~1 s, each call returns while that kernel still runs: the stream is still busy
+    (Stream.query() is False) and the call took a small fraction of the spin.  The handle is a
+    config-3 one without the equality workspace, the case whose bounds scan once read the
+    device flag back (round 5): the rows are now scanned on the device and the class pair is
+    gated by the flag with no host round trip.  The results equal an unobstructed run's."""
+    import time
+    import torch
+    from nmpc_amd import config_spec
+
+    spec = config_spec(3)
+    s = _solver(spec)
+    B, K = 64, 2
+    P, bnd, vt, wt = _closed_loop_inputs(spec, B, seed=31)
+    f64 = dict(dtype=torch.float64, device="cuda")
+    st = torch.cuda.Stream()
+
+    def outs():
+        return {"x": torch.empty(B, spec.nw, **f64), "f": torch.empty(B, **f64),
+                "status": torch.empty(B, dtype=torch.int32, device="cuda"),
+                "iters": torch.empty(B, dtype=torch.int32, device="cuda")}
+
+    def hists():
+        return {"u": torch.empty(K, B, 6, **f64), "status": torch.empty(K, B, dtype=torch.int32, device="cuda")}
+
+    w0, p0 = torch.zeros(B, spec.nw, **f64), torch.tensor(P, **f64)
+    # unobstructed runs first: they also size the workspace and the scheduler state (an
+    # allocation may synchronise; a sized handle only enqueues)
+    ref_o, ref_h = outs(), hists()
+    s.solve_device(w0, *bnd, p0, ref_o, stream=st)
+    s.closed_loop_device(K, *bnd, p0.clone(), w0.clone(), vt, wt, ref_h, stream=st, check=False)
+    torch.cuda.synchronize()
+    assert s.memory_info()["ws_eq_bytes"] == 0
+    # calibrate the spin kernel (torch.cuda._sleep: clock cycles) to ~1 s
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    with torch.cuda.stream(st):
+        e0.record(st); torch.cuda._sleep(1 << 24); e1.record(st)
+    torch.cuda.synchronize()
+    per_cycle_ms = e0.elapsed_time(e1) / (1 << 24)
+    cycles = int(min(max(1000.0 / max(per_cycle_ms, 1e-12), float(1 << 24)), float(1 << 36)))
+    for what in ("solve", "closed_loop"):
+        o, hh = outs(), hists()
+        pc, wc = p0.clone(), w0.clone()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        with torch.cuda.stream(st):
+            e0.record(st)
+            torch.cuda._sleep(cycles)
+            e1.record(st)
+        t0 = time.perf_counter()
+        if what == "solve":
+            s.solve_device(w0, *bnd, p0, o, stream=st)
+        else:
+            s.closed_loop_device(K, *bnd, pc, wc, vt, wt, hh, stream=st, check=False)
+        call_ms = (time.perf_counter() - t0) * 1e3
+        busy = not st.query()
+        torch.cuda.synchronize()
+        spin_ms = e0.elapsed_time(e1)
+        print(f"{what}: call {call_ms:.2f} ms, spin {spin_ms:.0f} ms, stream busy after the call: {busy}")
+        assert spin_ms > 300.0
+        assert busy and call_ms < 0.25 * spin_ms, (what, call_ms, spin_ms)
+        if what == "solve":
+            for k in o:
+                np.testing.assert_array_equal(o[k].cpu().numpy(), ref_o[k].cpu().numpy(), err_msg=k)
+        else:
+            s.check_closed_loop(B, K)
+            for k in hh:
+                np.testing.assert_array_equal(hh[k].cpu().numpy(), ref_h[k].cpu().numpy(), err_msg=k)
+
+
+def test_speculative_restoration_pairs_are_bitwise_neutral(monkeypatch):
+    """The restoration line search of the LDS-row class forms each new trial together with
+    the next backtracking trial (Solver::kSpec: rollout2 / eval_fg2 on lanes 32 + k, the
+    second trial's X, rows and objective parked in lam, dms and spec_f), and a later
+    from_pair acceptance -- possibly after a failed second-order correction in between --
+    takes that parked trial.  Against a handle whose trials are all formed alone
+    (NMPC_NO_SPEC=1 at nmpc_create, Params::nospec), the bench's whole config-3 workload
+    (4,096 scenarios x 20 closed-loop steps from u = 0: the restoration-heavy chains that
+    bound the launch, with their SOC blocks) gives bitwise the same histories."""
+    import torch
+    from nmpc_amd import config_spec
+
+    spec = config_spec(3)
+    B, K = 4096, 20
+    P, bnd, vt, wt = _closed_loop_inputs(spec, B, seed=1003)
+    f64 = dict(dtype=torch.float64, device="cuda")
+
+    def run():
+        s = _solver(spec)
+        hist = {"u": torch.empty(K, B, 6, **f64), "f": torch.empty(K, B, **f64),
+                "status": torch.empty(K, B, dtype=torch.int32, device="cuda"),
+                "iters": torch.empty(K, B, dtype=torch.int32, device="cuda")}
+        p, w = torch.tensor(P, **f64), torch.zeros(B, spec.nw, **f64)
+        s.closed_loop_device(K, *bnd, p, w, vt, wt, hist)
+        torch.cuda.synchronize()
+        return {k: v.cpu().numpy() for k, v in hist.items()}, p.cpu().numpy(), w.cpu().numpy()
+
+    a, pa, wa = run()
+    monkeypatch.setenv("NMPC_NO_SPEC", "1")
+    b, pb, wb = run()
+    st = a["status"]
+    print(f"iterations {int(a['iters'].sum())}, max_iter steps {int((st == -1).sum())}, "
+          f"infeasible {int((st == 2).sum())}")
+    assert int((st == -1).sum()) > 100  # restoration-heavy max_iter steps are in the workload
+    for k in a:
+        np.testing.assert_array_equal(a[k], b[k], err_msg=k)
+    np.testing.assert_array_equal(pa, pb)
+    np.testing.assert_array_equal(wa, wb)
+
+
 def test_shift_kernel_matches_reference_shift():
     import torch
     from nmpc_amd import make_spec, draw_scenarios

@@ -131,6 +131,7 @@ def test_equality_rows_closed_loop_matches_per_step_launches(extra):
            "status": torch.empty(B, dtype=torch.int32, device="cuda"),
            "iters": torch.empty(B, dtype=torch.int32, device="cuda")}
     ref = {"u": [], "f": [], "status": [], "iters": []}
+    s.reserve_equality(B)  # the device entry points never allocate it themselves
     for _ in range(K):
         s.solve_device(w1, *bnd, p1, out)
         ref["u"].append(out["x"][:, :6].clone())
@@ -222,14 +223,17 @@ def test_watchdog_stop_with_equality_rows_matches_oracle(case, last, skip):
 
 def test_equality_workspace_is_allocated_lazily():
     """The equality class's workspace (~840 KB per scenario: global rows up to N = 63 and the
-    128 x 128 Schur storage) is allocated only once a batch with equality rows is solved; a
-    config-3 handle whose batches have none holds its class's ~120 KB per scenario only.
-    Device-pointer batches: without the equality workspace the bounds are scanned and the
-    applicable class launched alone; once it exists, the gated pair runs -- the results are
-    bitwise the same either way, and an equality batch through the device path equals the
-    host path's solve of it."""
+    128 x 128 Schur storage) is allocated only when asked for; a config-3 handle whose batches
+    have none holds its class's ~120 KB per scenario only.
+    Device-pointer batches never allocate it (they never synchronise the host): without it a
+    batch with equality rows reports NMPC_STATUS_EQ_UNRESERVED (-102) per scenario with NaN x
+    and f, and a closed loop raises (scheduler_error bit 4); after reserve_equality(B) it
+    is solved, and a batch without equality rows gives bitwise the same results either way.
+    The host-array call allocates it on demand, and an equality batch through the device path
+    equals the host path's solve of it."""
     import torch
     from nmpc_amd import nlpsol, config_spec, draw_scenarios, make_spec, REFERENCE_OPTS
+    from nmpc_amd._lib import NmpcError, EQ_UNRESERVED
 
     f64 = dict(dtype=torch.float64, device="cuda")
     spec = config_spec(3)
@@ -247,7 +251,8 @@ def test_equality_workspace_is_allocated_lazily():
     assert mi["ws_per_scenario"] <= 130_000 < mi["ws_eq_per_scenario"]
 
     prob, p, lbx, ubx, lbg, ubg, row = _pinned_z_problem(0)
-    s = nlpsol("solver", "ipopt", make_spec("race_track_2", N=8, T=0.2), REFERENCE_OPTS)
+    spec8 = make_spec("race_track_2", N=8, T=0.2)
+    s = nlpsol("solver", "ipopt", spec8, REFERENCE_OPTS)
     Bs = 3
     pd = torch.tensor(np.tile(p, (Bs, 1)), **f64)
     x0 = torch.zeros(Bs, prob.nw, **f64)
@@ -264,12 +269,28 @@ def test_equality_workspace_is_allocated_lazily():
     lbg0, ubg0 = orc.bounds(prob)[2:]
     a1 = dev_solve(lbg0, ubg0)                      # no equality row: the class alone
     assert s.memory_info()["ws_eq_bytes"] == 0
-    e1 = dev_solve(lbg, ubg)                        # equality rows: the equality class, workspace now
+    e0 = dev_solve(lbg, ubg)                        # equality rows, nothing reserved: not solved
+    assert s.memory_info()["ws_eq_bytes"] == 0
+    assert np.all(e0["status"] == EQ_UNRESERVED) and np.all(np.isnan(e0["x"])) and np.all(np.isnan(e0["f"]))
+    # the closed loop reports it too (and raises on the synchronous path)
+    hq = {"status": torch.empty(2, Bs, dtype=torch.int32, device="cuda")}
+    bq = [torch.tensor(v, **f64) for v in (lbx, ubx, lbg, ubg)]
+    with pytest.raises(NmpcError, match="reserve_equality"):
+        s.closed_loop_device(2, *bq, pd.clone(), x0.clone(), torch.full((Bs,), 12.0, **f64),
+                             torch.full((Bs,), 0.01, **f64), hq)
+    assert np.all(hq["status"].cpu().numpy() == EQ_UNRESERVED)
+    s.reserve_equality(Bs)
     assert s.memory_info()["ws_eq_bytes"] == Bs * s.memory_info()["ws_eq_per_scenario"]
+    e1 = dev_solve(lbg, ubg)                        # equality rows: the equality class
     a2 = dev_solve(lbg0, ubg0)                      # the gated pair, decided on the device
     for k in a1:
         np.testing.assert_array_equal(a1[k], a2[k])
     h = s(x0=np.zeros(prob.nw), lbx=lbx, ubx=ubx, lbg=lbg, ubg=ubg, p=p)
     assert int(e1["status"][0]) == int(np.ravel(s.stats()["status_code"])[0]) == orc.SOLVE_SUCCEEDED
     np.testing.assert_array_equal(e1["x"][0], h["x"].ravel())
+    # the host-array call allocates the workspace on demand
+    s2 = nlpsol("solver", "ipopt", spec8, REFERENCE_OPTS)
+    h2 = s2(x0=np.zeros(prob.nw), lbx=lbx, ubx=ubx, lbg=lbg, ubg=ubg, p=p)
+    assert s2.memory_info()["ws_eq_bytes"] == s2.memory_info()["ws_eq_per_scenario"]
+    np.testing.assert_array_equal(h2["x"], h["x"])
     assert abs(float(h["g"].ravel()[row]) - lbg[row]) <= 1e-6

@@ -34,7 +34,9 @@ Three comparisons per run:
       passing on one side and missing tol by at most 100x on the other; at every step
       where the GPU's status or converged x differs, the GPU's (status, x) lies in the
       rounding variants' envelope there (some variant's status, and x within 1e-6 of that
-      variant's or no farther from the fixture's than that variant's); and the GPU changes
+      variant's or no farther from the fixture's than that variant's -- for an unconverged
+      status, no farther than UNCONV_SPREAD_FACTOR x the same-status variants' farthest);
+      and the GPU changes
       no more statuses than the variants and no more converged x than the compiled
       restatement does; measured regression floors besides.
       For every differing step the test prints which termination test decided and its
@@ -66,6 +68,11 @@ RUN_NAMES = ["nmpc_tt", "10_obstacles", "race_track_2", "matlab_nmpc_tt", "dynam
              "dynamic_obstacles_derived"]
 # (c): |GPU - fixture| of the whole-run FOV-error sum <= this x the largest |variant - fixture|
 FOV_SPREAD_FACTOR = 2.0
+# (a), unconverged steps (max_iter, restoration failure, infeasible): the GPU's last iterate
+# must lie within 1e-6 of a variant's with the same status, or no farther from the fixture's
+# x than this x the farthest same-status variant's (the scatter of rounding-level solvers
+# whose 100th iteration -- or failed restoration -- leaves them at different points)
+UNCONV_SPREAD_FACTOR = 2.0
 # Regression floors measured on the GPU (round 4, gpurun_out/r04z_tests.log), one step of
 # slack each: per step, statuses and iteration counts equal to the fixture's; chained, the
 # GPU loop's agreeing prefix (besides the rounding variants' part point minus one step).
@@ -215,12 +222,25 @@ def test_reference_run_per_step(name):
         vconv_i = np.isin(vs, (0, 1))
         dev_v = sp["step_dev_x"][:, i]  # each variant's deviation from the fixture's x
         conv_i = st[i] in (0, 1)
-        match = (vs == st[i]) & (~vconv_i | (ev <= TOL) | (ex[i] <= dev_v))
-        if not conv_i and not vconv_i.any():
-            match |= ev <= TOL
+        same_st = vs == st[i]
+        margin = ""
+        if conv_i:
+            match = same_st & ((ev <= TOL) | (ex[i] <= dev_v))
+        else:
+            # unconverged: a same-status variant's x within 1e-6, or the GPU's x inside the
+            # same-status variants' scatter around the fixture (UNCONV_SPREAD_FACTOR), printed
+            # as a named margin (round 6: status alone no longer admits such a step)
+            scatter = float(dev_v[same_st].max()) if same_st.any() else float("nan")
+            bound = UNCONV_SPREAD_FACTOR * scatter + TOL
+            match = same_st & ((ev <= TOL) | (ex[i] <= bound))
+            if not vconv_i.any():  # every solver unconverged: a variant's x under another failure status
+                match |= ev <= TOL
+            margin = (f"; unconverged-x margin: GPU {ex[i]:.2e} from the fixture vs bound {bound:.2e} "
+                      f"({UNCONV_SPREAD_FACTOR:g} x the same-status variants' farthest {scatter:.2e}), "
+                      f"nearest same-status variant {float(ev[same_st].min()) if same_st.any() else float('nan'):.2e}")
         print(f"  envelope step {i}: GPU status {st[i]}, x dev from the fixture {ex[i]:.1e}; variants status "
               f"{[int(v) for v in vs]}, their x dev from the fixture {[f'{e:.1e}' for e in dev_v]}, from the GPU's "
-              f"{[f'{e:.1e}' for e in ev]} -> {'within' if match.any() else 'OUTSIDE'}")
+              f"{[f'{e:.1e}' for e in ev]} -> {'within' if match.any() else 'OUTSIDE'}{margin}")
         if not match.any():
             outside.append(int(i))
     assert not outside, f"GPU result at these steps lies outside every rounding variant's: {outside}"
