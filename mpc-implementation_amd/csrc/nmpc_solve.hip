@@ -329,6 +329,31 @@ __device__ __forceinline__ double rsq(double x) {
   return fma(y, r, y);
 }
 __device__ __forceinline__ float rsq(float x) { return __builtin_amdgcn_rsqf(x); }  // v_rsq_f32, ~1 ulp
+// fp64 quotient a / b by the compiler's own sequence without its range fix-ups: the same
+// v_rcp_f64 estimate, two Newton steps, q = a r and one Markstein correction as LLVM's
+// fdiv lowering, minus v_div_scale (x2), v_div_fmas and v_div_fixup, which act only when an
+// operand or the quotient is out of range (exponents near the limits, zero, inf, NaN).  So
+// bitwise a / b for finite non-zero operands of moderate range -- slacks, multipliers,
+// pivots, distances, step components -- which is what every call site divides; where a
+// caller's operand can be 0 or inf (a missing bound, a zero step component) its result is
+// discarded by the caller's guard, as a / b's was.  Three fewer instructions per division,
+// two of them on the dependence chain.  NMPC_FDIV=0: plain a / b.
+#ifndef NMPC_FDIV
+#define NMPC_FDIV 1
+#endif
+__device__ __forceinline__ double qd(double a, double b) {
+  if constexpr (NMPC_FDIV) {
+    double r = __builtin_amdgcn_rcp(b);
+    double e = fma(-b, r, 1.0);
+    r = fma(r, e, r);
+    e = fma(-b, r, 1.0);
+    r = fma(r, e, r);
+    const double q = a * r;
+    return fma(fma(-b, q, a), r, q);
+  } else {
+    return a / b;
+  }
+}
 __device__ __forceinline__ float readlane_d(float v, int l) {
   return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
 }
@@ -704,6 +729,8 @@ struct Solver {
     const double bb = (z * t5p - z * t5m) / 2;
     const double c7 = cos(x[7]), s7 = sin(x[7]);
     const double a2 = a * a, b2 = bb * bb;
+    // (the compiler's divisions: with qd() the objective value moved in its last bit at a few
+    // points of the round-6 bitwise A/B -- cause not isolated -- so they stay)
     const double A = (c7 * c7) / a2 + (s7 * s7) / b2;
     const double Bq = 2 * c7 * s7 * ((1 / a2) - (1 / b2));
     const double C = (s7 * s7) / a2 + (c7 * c7) / b2;
@@ -952,7 +979,7 @@ struct Solver {
         const double r1 = c * ex + sn * ey;
         const double r2 = sn * ex - c * ey;
         double u1[6], u2[6], gr1[6], gr2[6], ge1[6], ge2[6];
-        const double ia = 1.0 / a, ib = 1.0 / bb;
+        const double ia = qd(1.0, a), ib = qd(1.0, bb);
         const double e1 = r1 * ia, e2 = r2 * ib;
 #pragma unroll
         for (int q = 0; q < 6; ++q) {
@@ -965,7 +992,7 @@ struct Solver {
         }
         const double ddx = x - xt, ddy = yy - yt;
         const double dd = TC ? tk[10] : sqrt(ddx * ddx + ddy * ddy);
-        const double idd = 1.0 / dd;
+        const double idd = qd(1.0, dd);
         const double id3 = idd * idd * idd;
         const double w1 = rvars[30], w2 = rvars[31];  // this scenario's cost weights
         // gradient
@@ -2311,14 +2338,14 @@ struct Solver {
       const double lo = dl[r], hi = du[r], sr = s[r];
       const double dd = eqlo(lo) ? 0.0 : jd + dms[r];  // equality rows: the slack stays at the target
       if (on) dso[r] = dd;
-      const double al = (-tau_ * (sr - lo)) / dd, au = (-tau_ * (hi - sr)) / (-dd);
+      const double al = qd(-tau_ * (sr - lo), dd), au = qd(-tau_ * (hi - sr), -dd);
       if (on && hasl(lo) && dd < 0) a = fmin(a, al);
       if (on && hasu(hi) && -dd < 0) a = fmin(a, au);
     });
     for (int i = lanef(); i < nw; i += WAVE) {
       const double dx = dUs[i];
-      if (hasl(xl[i]) && dx < 0) a = fmin(a, (-tau_ * (U[i] - xl[i])) / dx);
-      if (hasu(xu[i]) && -dx < 0) a = fmin(a, (-tau_ * (xu[i] - U[i])) / (-dx));
+      if (hasl(xl[i]) && dx < 0) a = fmin(a, qd(-tau_ * (U[i] - xl[i]), dx));
+      if (hasu(xu[i]) && -dx < 0) a = fmin(a, qd(-tau_ * (xu[i] - U[i]), -dx));
     }
     a = wmin(a);
     STAMP1(PH_ROWSTEP);
@@ -2355,15 +2382,15 @@ struct Solver {
       const double dsr = eqlo(lo) ? 0.0 : jd + (dr - sr);
       if (on) ds[r] = dsr;
       const bool hl = hasl(lo), hu = hasu(hi);
-      const double gs = -(hl ? mu_ / (sr - lo) : 0.0) + (hu ? mu_ / (hi - sr) : 0.0) +
+      const double gs = -(hl ? qd(mu_, sr - lo) : 0.0) + (hu ? qd(mu_, hi - sr) : 0.0) +
                         kd * mu_ * ((hl && !hu ? 1.0 : 0.0) - (hu && !hl ? 1.0 : 0.0));
       if (on) {
         th += fabs(dr - sr);
         g += gs * dsr;
-        msv = fmax(msv, fabs(dsr / (1.0 + fabs(sr))));
+        msv = fmax(msv, fabs(qd(dsr, 1.0 + fabs(sr))));
       }
       // fraction to the boundary of this step: primal (frac_to_bound_x) ...
-      const double al = (-tau_ * (sr - lo)) / dsr, au = (-tau_ * (hi - sr)) / (-dsr);
+      const double al = qd(-tau_ * (sr - lo), dsr), au = qd(-tau_ * (hi - sr), -dsr);
       if (on && hl && dsr < 0) ap = fmin(ap, al);
       if (on && hu && -dsr < 0) ap = fmin(ap, au);
       // ... and dual (dual_frac_to_bound_x: dv_s with mu_)
@@ -2371,7 +2398,7 @@ struct Solver {
       double a1 = 0.0, a2 = 0.0;
       if (hl) { const double iS = rcp(sr - lo); a1 = mu_ * iS - vlr - vlr * iS * dsr; }
       if (hu) { const double iS = rcp(hi - sr); a2 = mu_ * iS - vur + vur * iS * dsr; }
-      const double b1 = (-tau_ * vlr) / a1, b2 = (-tau_ * vur) / a2;
+      const double b1 = qd(-tau_ * vlr, a1), b2 = qd(-tau_ * vur, a2);
       if (on && hl && a1 < 0) ad = fmin(ad, b1);
       if (on && hu && a2 < 0) ad = fmin(ad, b2);
     });
@@ -2388,24 +2415,24 @@ struct Solver {
     row_rs(r, D, rs);
     const double kd = P->o.kappa_d;
     const double pr = pR[r], nr = nR[r];
-    const double ip = 1.0 / pr, in_ = 1.0 / nr;
+    const double ip = qd(1.0, pr), in_ = qd(1.0, nr);
     Sp = zpR[r] * ip + delta;
     Sn = znR[r] * in_ + delta;
     rp = rho - y[r] - mu * ip + kd * mu;
     rn = rho + y[r] - mu * in_ + kd * mu;
     const double c = soc ? cms[r] : d[r] - s[r] - pr + nr;
-    const double iSp = 1.0 / Sp, iSn = 1.0 / Sn;
-    const double den = 1.0 / (1.0 + D * (iSp + iSn));
+    const double iSp = qd(1.0, Sp), iSn = qd(1.0, Sn);
+    const double den = qd(1.0, 1.0 + D * (iSp + iSn));
     Dt = D * den;
     Dr = Dt * (c + rp * iSp - rn * iSn) + rs * den;
     if (eqr(r)) {  // equality row: no slack, the D -> infinity limit
-      Dt = 1.0 / (iSp + iSn);
+      Dt = qd(1.0, iSp + iSn);
       Dr = Dt * (c + rp * iSp - rn * iSn);
     }
   }
   __device__ __forceinline__ double dr2(int i) const {  // D_R^2 = 1/max(1,|x_R|)^2
     const double a = fmax(1.0, fabs(UR[i]));
-    return 1.0 / (a * a);
+    return qd(1.0, a * a);
   }
   // restoration step rows: dy, dp, dn, ds (= J dx + c - dp + dn); for the Newton
   // direction also theta_R and the slack/p/n part of grad(phi_R)^T d
@@ -2436,21 +2463,24 @@ struct Solver {
       const double pr = pR[r], nr = nR[r];
       const double c = soc ? cms[r] : d[r] - s[r] - pr + nr;
       const double dyv = Dt * jd + Dr;
-      const double dpv = (dyv - rp) / Sp, dnv = (-dyv - rn) / Sn;
+      const double dpv = qd(dyv - rp, Sp), dnv = qd(-dyv - rn, Sn);
       const double dsv = eqr(r) ? 0.0 : jd + c - dpv + dnv;
       if (on) { dso[r] = dsv; dpo[r] = dpv; dno[r] = dnv; dyo[r] = dyv; }
       const double lo = dl[r], hi = du[r], sr = s[r];
       const bool hl = hasl(lo), hu = hasu(hi);
       // primal fraction to the boundary (frac_to_bound_x rows + the p, n bounds)
       {
-        const double al = (-tau_ * (sr - lo)) / dsv, au = (-tau_ * (hi - sr)) / (-dsv);
+        const double al = qd(-tau_ * (sr - lo), dsv), au = qd(-tau_ * (hi - sr), -dsv);
         if (on && hl && dsv < 0) ap = fmin(ap, al);
         if (on && hu && -dsv < 0) ap = fmin(ap, au);
-        const double bp = (-tau_ * pr) / dpv, bn = (-tau_ * nr) / dnv;
+        const double bp = qd(-tau_ * pr, dpv), bn = qd(-tau_ * nr, dnv);
         if (on && dpv < 0) ap = fmin(ap, bp);
         if (on && dnv < 0) ap = fmin(ap, bn);
       }
       if (!soc) {
+        // (plain divisions here: with qd() these two lines alone change the restoration
+        // line search's results -- the one place the bitwise A/B of round 6 found one, cause
+        // not isolated -- so they keep the compiler's division)
         const double gs = -(hl ? mu / (sr - lo) : 0.0) + (hu ? mu / (hi - sr) : 0.0) +
                           kd * mu * ((hl && !hu ? 1.0 : 0.0) - (hu && !hl ? 1.0 : 0.0));
         const double gr = gs * dsv + (rho - mu / pr + kd * mu) * dpv + (rho - mu / nr + kd * mu) * dnv;
@@ -2464,12 +2494,12 @@ struct Solver {
         double a1 = 0.0, a2 = 0.0;
         if (hl) { const double iS = rcp(sr - lo); a1 = mu * iS - vlr - vlr * iS * dsv; }
         if (hu) { const double iS = rcp(hi - sr); a2 = mu * iS - vur + vur * iS * dsv; }
-        const double b1 = (-tau_ * vlr) / a1, b2 = (-tau_ * vur) / a2;
+        const double b1 = qd(-tau_ * vlr, a1), b2 = qd(-tau_ * vur, a2);
         if (on && hl && a1 < 0) ad = fmin(ad, b1);
         if (on && hu && a2 < 0) ad = fmin(ad, b2);
-        const double dzp = mu / pr - zp - (zp / pr) * dpv;
-        const double dzn = mu / nr - zn - (zn / nr) * dnv;
-        const double cp = (-tau_ * zp) / dzp, cn = (-tau_ * zn) / dzn;
+        const double dzp = qd(mu, pr) - zp - qd(zp, pr) * dpv;
+        const double dzn = qd(mu, nr) - zn - qd(zn, nr) * dnv;
+        const double cp = qd(-tau_ * zp, dzp), cn = qd(-tau_ * zn, dzn);
         if (on && dzp < 0) ad = fmin(ad, cp);
         if (on && dzn < 0) ad = fmin(ad, cn);
       }
@@ -2593,7 +2623,7 @@ struct Solver {
     double b = 1.0;  // p, n bounds in the same pass (min is order-free)
     const double a = frac_to_bound_x(tau_, dUs, dss, [&](int r, bool on) {
       const double dp = dps[r], dn = dns[r], pr = pR[r], nr = nR[r];
-      const double bp = (-tau_ * pr) / dp, bn = (-tau_ * nr) / dn;
+      const double bp = qd(-tau_ * pr, dp), bn = qd(-tau_ * nr, dn);
       if (on && dp < 0) b = fmin(b, bp);
       if (on && dn < 0) b = fmin(b, bn);
     });
@@ -2604,9 +2634,9 @@ struct Solver {
     double b = 1.0;
     const double a = dual_frac_to_bound_x(tau_, dUs, dss, [&](int r, bool on) {
       const double pr = pR[r], nr = nR[r], zp = zpR[r], zn = znR[r], dp = dps[r], dn = dns[r];
-      const double dzp = mu / pr - zp - (zp / pr) * dp;
-      const double dzn = mu / nr - zn - (zn / nr) * dn;
-      const double bp = (-tau_ * zp) / dzp, bn = (-tau_ * zn) / dzn;
+      const double dzp = qd(mu, pr) - zp - qd(zp, pr) * dp;
+      const double dzn = qd(mu, nr) - zn - qd(zn, nr) * dn;
+      const double bp = qd(-tau_ * zp, dzp), bn = qd(-tau_ * zn, dzn);
       if (on && dzp < 0) b = fmin(b, bp);
       if (on && dzn < 0) b = fmin(b, bn);
     });
@@ -2625,12 +2655,12 @@ struct Solver {
     double a = 1.0;
     ctrls([&](int i, bool on) {  // (a repeated last entry leaves a minimum unchanged)
       const double dx = dUs[i];
-      if (hasl(xl[i]) && dx < 0) a = fmin(a, (-tau_ * (U[i] - xl[i])) / dx);
-      if (hasu(xu[i]) && -dx < 0) a = fmin(a, (-tau_ * (xu[i] - U[i])) / (-dx));
+      if (hasl(xl[i]) && dx < 0) a = fmin(a, qd(-tau_ * (U[i] - xl[i]), dx));
+      if (hasu(xu[i]) && -dx < 0) a = fmin(a, qd(-tau_ * (xu[i] - U[i]), -dx));
     });
     rows([&](int r, bool on) {
       const double dd = dss[r], sr = s[r], lo = dl[r], hi = du[r];
-      const double al = (-tau_ * (sr - lo)) / dd, au = (-tau_ * (hi - sr)) / (-dd);
+      const double al = qd(-tau_ * (sr - lo), dd), au = qd(-tau_ * (hi - sr), -dd);
       if (on && hasl(lo) && dd < 0) a = fmin(a, al);
       if (on && hasu(hi) && -dd < 0) a = fmin(a, au);
       extra(r, on);
@@ -2672,8 +2702,8 @@ struct Solver {
     ctrls([&](int i, bool on) {
       double a1, a2;
       dz_x(i, dUs[i], a1, a2);
-      if (hasl(xl[i]) && a1 < 0) a = fmin(a, (-tau_ * zl[i]) / a1);
-      if (hasu(xu[i]) && a2 < 0) a = fmin(a, (-tau_ * zu[i]) / a2);
+      if (hasl(xl[i]) && a1 < 0) a = fmin(a, qd(-tau_ * zl[i], a1));
+      if (hasu(xu[i]) && a2 < 0) a = fmin(a, qd(-tau_ * zu[i], a2));
     });
     rows([&](int r, bool on) {
       const double sr = s[r], lo = dl[r], hi = du[r], vlr = vl[r], vur = vu[r], dsv = dss[r];
@@ -2681,7 +2711,7 @@ struct Solver {
       double a1 = 0.0, a2 = 0.0;  // dv_s with the loads hoisted
       if (hl) { const double iS = rcp(sr - lo); a1 = mu * iS - vlr - vlr * iS * dsv; }
       if (hu) { const double iS = rcp(hi - sr); a2 = mu * iS - vur + vur * iS * dsv; }
-      const double b1 = (-tau_ * vlr) / a1, b2 = (-tau_ * vur) / a2;
+      const double b1 = qd(-tau_ * vlr, a1), b2 = qd(-tau_ * vur, a2);
       if (on && hl && a1 < 0) a = fmin(a, b1);
       if (on && hu && a2 < 0) a = fmin(a, b2);
       extra(r, on);
@@ -3083,8 +3113,8 @@ __device__ __forceinline__ void resto_phase(const Params* __restrict__ prm, doub
           const bool hl = S.hasl(S.xl[i]), hu = S.hasu(S.xu[i]);
           const double Sl = hl ? S.U[i] - S.xl[i] : 1.0, Su = hu ? S.xu[i] - S.U[i] : 1.0;
           const double w2 = S.etaR * S.dr2(i);
-          const double sg = w2 + ((hl ? S.zl[i] / Sl : 0.0) + (hu ? S.zu[i] / Su : 0.0));
-          const double rr = w2 * (S.U[i] - S.UR[i]) + (-(hl ? muR4 / Sl : 0.0) + (hu ? muR4 / Su : 0.0) +
+          const double sg = w2 + ((hl ? qd(S.zl[i], Sl) : 0.0) + (hu ? qd(S.zu[i], Su) : 0.0));
+          const double rr = w2 * (S.U[i] - S.UR[i]) + (-(hl ? qd(muR4, Sl) : 0.0) + (hu ? qd(muR4, Su) : 0.0) +
                             kd * muR4 * ((hl && !hu ? 1.0 : 0.0) - (hu && !hl ? 1.0 : 0.0)));
           if (on) { S.sigx[i] = sg; S.ru[i] = rr; }
         });
@@ -3129,12 +3159,12 @@ __device__ __forceinline__ void resto_phase(const Params* __restrict__ prm, doub
             const double gi = S.ru[i] * du_;
             if (on) g += gi;
             const double ui = S.U[i], xli = S.xl[i], xui = S.xu[i];
-            if (S.hasl(xli) && du_ < 0) ap = fmin(ap, (-tauR * (ui - xli)) / du_);
-            if (S.hasu(xui) && -du_ < 0) ap = fmin(ap, (-tauR * (xui - ui)) / (-du_));
+            if (S.hasl(xli) && du_ < 0) ap = fmin(ap, qd(-tauR * (ui - xli), du_));
+            if (S.hasu(xui) && -du_ < 0) ap = fmin(ap, qd(-tauR * (xui - ui), -du_));
             double a1, a2;
             S.dz_x(i, du_, a1, a2);
-            if (S.hasl(xli) && a1 < 0) ad = fmin(ad, (-tauR * S.zl[i]) / a1);
-            if (S.hasu(xui) && a2 < 0) ad = fmin(ad, (-tauR * S.zu[i]) / a2);
+            if (S.hasl(xli) && a1 < 0) ad = fmin(ad, qd(-tauR * S.zl[i], a1));
+            if (S.hasu(xui) && a2 < 0) ad = fmin(ad, qd(-tauR * S.zu[i], a2));
           });
           V[15] = wsum(th);
           V[16] = wsum(g);
@@ -3321,8 +3351,8 @@ __device__ __forceinline__ void resto_phase(const Params* __restrict__ prm, doub
               S.row_step_resto(S.dX, true, S.ds2, S.dp2R, S.dn2R, S.dy2R, t0, t1, tauR, ap, u1);
               S.ctrls([&](int i, bool) {  // frac_to_bound_resto's control part
                 const double du_ = S.dU2[i], ui = S.U[i], xli = S.xl[i], xui = S.xu[i];
-                if (S.hasl(xli) && du_ < 0) ap = fmin(ap, (-tauR * (ui - xli)) / du_);
-                if (S.hasu(xui) && -du_ < 0) ap = fmin(ap, (-tauR * (xui - ui)) / (-du_));
+                if (S.hasl(xli) && du_ < 0) ap = fmin(ap, qd(-tauR * (ui - xli), du_));
+                if (S.hasu(xui) && -du_ < 0) ap = fmin(ap, qd(-tauR * (xui - ui), -du_));
               });
               a_soc = wmin(ap);
               dsp = S.ds2; dpp = S.dp2R; dnp = S.dn2R;
@@ -3372,9 +3402,9 @@ __device__ __forceinline__ void resto_phase(const Params* __restrict__ prm, doub
             S.dz_x(i, dUa[i], dzl, dzu);
             double nzl = S.zl[i] + ad * dzl, nzu = S.zu[i] + ad * dzu;
             const double un = S.Ut[i];
-            if (S.hasl(S.xl[i])) { const double Sn = un - S.xl[i]; nzl = fmax(fmin(nzl, ks * muA / Sn), muA / (ks * Sn)); }
+            if (S.hasl(S.xl[i])) { const double Sn = un - S.xl[i]; nzl = fmax(fmin(nzl, qd(ks * muA, Sn)), qd(muA, ks * Sn)); }
             else nzl = 0.0;
-            if (S.hasu(S.xu[i])) { const double Sn = S.xu[i] - un; nzu = fmax(fmin(nzu, ks * muA / Sn), muA / (ks * Sn)); }
+            if (S.hasu(S.xu[i])) { const double Sn = S.xu[i] - un; nzu = fmax(fmin(nzu, qd(ks * muA, Sn)), qd(muA, ks * Sn)); }
             else nzu = 0.0;
             if (on) { S.zl[i] = nzl; S.zu[i] = nzu; S.U[i] = un; }
           });
@@ -3389,18 +3419,18 @@ __device__ __forceinline__ void resto_phase(const Params* __restrict__ prm, doub
             double dvl = 0.0, dvu = 0.0;  // dv_s with the loads hoisted
             if (hl) { const double iS = rcp(sr - lo); dvl = S.mu * iS - vlr - vlr * iS * dsr; }
             if (hu) { const double iS = rcp(hi - sr); dvu = S.mu * iS - vur + vur * iS * dsr; }
-            const double dzp = dmuR / pr - zp - (zp / pr) * dpr;
-            const double dzn = dmuR / nr - zn - (zn / nr) * dnr;
+            const double dzp = qd(dmuR, pr) - zp - qd(zp, pr) * dpr;
+            const double dzn = qd(dmuR, nr) - zn - qd(zn, nr) * dnr;
             const double sn = sr + aP * dsr;
             const double pn = pr + aP * dpr, nn = nr + aP * dnr;
             double nvl = vlr + ad * dvl, nvu = vur + ad * dvu;
-            if (hl) { const double Sn = sn - lo; nvl = fmax(fmin(nvl, ks * muR / Sn), muR / (ks * Sn)); }
+            if (hl) { const double Sn = sn - lo; nvl = fmax(fmin(nvl, qd(ks * muR, Sn)), qd(muR, ks * Sn)); }
             else nvl = 0.0;
-            if (hu) { const double Sn = hi - sn; nvu = fmax(fmin(nvu, ks * muR / Sn), muR / (ks * Sn)); }
+            if (hu) { const double Sn = hi - sn; nvu = fmax(fmin(nvu, qd(ks * muR, Sn)), qd(muR, ks * Sn)); }
             else nvu = 0.0;
             const double nzp = zp + ad * dzp, nzn = zn + ad * dzn;
-            const double zpn = fmax(fmin(nzp, ks * muR / pn), muR / (ks * pn));
-            const double znn = fmax(fmin(nzn, ks * muR / nn), muR / (ks * nn));
+            const double zpn = fmax(fmin(nzp, qd(ks * muR, pn)), qd(muR, ks * pn));
+            const double znn = fmax(fmin(nzn, qd(ks * muR, nn)), qd(muR, ks * nn));
             const double t = fabs(dtr - sn);
             if (on) {
               S.zpR[r] = zpn; S.znR[r] = znn;
@@ -3637,17 +3667,28 @@ __device__ __forceinline__ int solve_one(Solver<CAP>& S, const Params* __restric
     S.df = fmax(dfv, o.nlp_scaling_min_value);
     // Jacobian row maxima: J rows = G_k Z_k, Z_k[:,u_j] = (I + sum_{l=j+1}^{k-1} E_l) B_j
     if (status == 0) {
+      // (every array below has a compile-time size and is indexed by unrolled loop counters
+      // only -- box rows rb[0..4], obstacle rows ro[q] -- so none of them lives in scratch)
+      constexpr int MO = CAP::mmax;  // obstacle rows per stage <= m - nb <= mmax
       const int k = S.lanef();
-      double rmax[5 + NMPC_MAX_OBS];
-      const int nb = S.nb;
-      for (int i = 0; i < m; ++i) rmax[i] = 0.0;
+      const int nb = S.nb, nobs = S.nobs;
+      double rb[5], ro[MO];
+#pragma unroll
+      for (int i = 0; i < 5; ++i) rb[i] = 0.0;
+#pragma unroll
+      for (int q = 0; q < MO; ++q) ro[q] = 0.0;
       if (k <= N && k >= 1) {
         const LDS double* xk = S.X + k * 8;
-        double gxo[NMPC_MAX_OBS], gyo[NMPC_MAX_OBS];
-        for (int q = 0; q < S.nobs; ++q) {
-          const double ddx = xk[0] - S.obx[q], ddy = xk[1] - S.oby[q];
-          const double dd = sqrt(ddx * ddx + ddy * ddy);
-          gxo[q] = -(ddx / dd); gyo[q] = -(ddy / dd);
+        double gxo[MO], gyo[MO];
+#pragma unroll
+        for (int q = 0; q < MO; ++q) {
+          if (q < nobs) {
+            const double ddx = xk[0] - S.obx[q], ddy = xk[1] - S.oby[q];
+            const double dd = sqrt(ddx * ddx + ddy * ddy);
+            gxo[q] = -(ddx / dd); gyo[q] = -(ddy / dd);
+          } else {
+            gxo[q] = 0.0; gyo[q] = 0.0;
+          }
         }
         double e03 = 0, e04 = 0, e13 = 0, e14 = 0, e23 = 0;  // sums over l in (j, k)
         const double T = S.T;
@@ -3658,30 +3699,44 @@ __device__ __forceinline__ int solve_one(Solver<CAP>& S, const Params* __restric
           const int fmj = S.nfix > 0 ? S.fixm[j] : 0;
           auto col = [&](int c, double v) { return ((fmj >> c) & 1) ? 0.0 : fabs(v); };
           // rows z, theta, x5, x6, x7
-          rmax[0] = fmax(rmax[0], fmax(col(0, b20), col(1, T * e23)));
-          rmax[1] = fmax(rmax[1], col(1, T));
+          rb[0] = fmax(rb[0], fmax(col(0, b20), col(1, T * e23)));
+          rb[1] = fmax(rb[1], col(1, T));
           if (nb == 5) {  // gimbal rows x5, x6, x7
-            rmax[2] = fmax(rmax[2], col(3, T));
-            rmax[3] = fmax(rmax[3], col(4, T));
-            rmax[4] = fmax(rmax[4], col(5, T));
+            rb[2] = fmax(rb[2], col(3, T));
+            rb[3] = fmax(rb[3], col(4, T));
+            rb[4] = fmax(rb[4], col(5, T));
           }
-          for (int q = 0; q < S.nobs; ++q) {
-            const double jv = gxo[q] * b00 + gyo[q] * b10;
-            const double jt = T * (gxo[q] * e03 + gyo[q] * e13);
-            const double jp = T * (gxo[q] * e04 + gyo[q] * e14);
-            rmax[nb + q] = fmax(rmax[nb + q], fmax(col(0, jv), fmax(col(1, jt), col(2, jp))));
+#pragma unroll
+          for (int q = 0; q < MO; ++q) {
+            if (q < nobs) {
+              const double jv = gxo[q] * b00 + gyo[q] * b10;
+              const double jt = T * (gxo[q] * e03 + gyo[q] * e13);
+              const double jp = T * (gxo[q] * e04 + gyo[q] * e14);
+              ro[q] = fmax(ro[q], fmax(col(0, jv), fmax(col(1, jt), col(2, jp))));
+            }
           }
           e03 += E03; e04 += E04; e13 += E13; e14 += E14; e23 += E23;
         }
       }
-      double amax = 0.0;
-      for (int i = 0; i < m; ++i) amax = fmax(amax, rmax[i]);
+      double amax = 0.0;  // (the rows in their order i = 0..m-1: box rows, then obstacles)
+#pragma unroll
+      for (int i = 0; i < 5; ++i)
+        if (i < nb) amax = fmax(amax, rb[i]);
+#pragma unroll
+      for (int q = 0; q < MO; ++q)
+        if (q < nobs) amax = fmax(amax, ro[q]);
       amax = wmax(amax);
       if (amax > o.nlp_scaling_max_gradient && k <= N) {
-        for (int i = 0; i < m; ++i) {
-          double dcv = rmax[i] > 0 ? fmin(1.0, o.nlp_scaling_max_gradient / rmax[i]) : 1.0;
-          S.dc[k * m + i] = fmax(dcv, o.nlp_scaling_min_value);
-        }
+        auto dcv = [&](double rm) {
+          const double v = rm > 0 ? fmin(1.0, o.nlp_scaling_max_gradient / rm) : 1.0;
+          return fmax(v, o.nlp_scaling_min_value);
+        };
+#pragma unroll
+        for (int i = 0; i < 5; ++i)
+          if (i < nb) S.dc[k * m + i] = dcv(rb[i]);
+#pragma unroll
+        for (int q = 0; q < MO; ++q)
+          if (q < nobs) S.dc[k * m + nb + q] = dcv(ro[q]);
       }
       sync();
     }
@@ -3919,8 +3974,8 @@ __device__ __forceinline__ int solve_one(Solver<CAP>& S, const Params* __restric
     S.ctrls([&](int i, bool on) {
       const bool hl = S.hasl(S.xl[i]), hu = S.hasu(S.xu[i]);
       const double Sl = hl ? S.U[i] - S.xl[i] : 1.0, Su = hu ? S.xu[i] - S.U[i] : 1.0;
-      const double sg = (hl ? S.zl[i] / Sl : 0.0) + (hu ? S.zu[i] / Su : 0.0);
-      const double rr = -(hl ? mu / Sl : 0.0) + (hu ? mu / Su : 0.0) +
+      const double sg = (hl ? qd(S.zl[i], Sl) : 0.0) + (hu ? qd(S.zu[i], Su) : 0.0);
+      const double rr = -(hl ? qd(mu, Sl) : 0.0) + (hu ? qd(mu, Su) : 0.0) +
                         o.kappa_d * mu * ((hl && !hu ? 1.0 : 0.0) - (hu && !hl ? 1.0 : 0.0));
       if (on) { S.sigx[i] = sg; S.ru[i] = rr; }
     });
@@ -3988,14 +4043,14 @@ __device__ __forceinline__ int solve_one(Solver<CAP>& S, const Params* __restric
         const double du_ = S.dU[i];
         const double gi = S.ru[i] * du_;
         if (on) g += gi;
-        mx = fmax(mx, fabs(du_ / (1.0 + fabs(S.U[i]))));
+        mx = fmax(mx, fabs(qd(du_, 1.0 + fabs(S.U[i]))));
         const double ui = S.U[i], xli = S.xl[i], xui = S.xu[i];
-        if (S.hasl(xli) && du_ < 0) ap = fmin(ap, (-tau * (ui - xli)) / du_);
-        if (S.hasu(xui) && -du_ < 0) ap = fmin(ap, (-tau * (xui - ui)) / (-du_));
+        if (S.hasl(xli) && du_ < 0) ap = fmin(ap, qd(-tau * (ui - xli), du_));
+        if (S.hasu(xui) && -du_ < 0) ap = fmin(ap, qd(-tau * (xui - ui), -du_));
         double a1, a2;
         S.dz_x(i, du_, a1, a2);
-        if (S.hasl(xli) && a1 < 0) ad = fmin(ad, (-tau * S.zl[i]) / a1);
-        if (S.hasu(xui) && a2 < 0) ad = fmin(ad, (-tau * S.zu[i]) / a2);
+        if (S.hasl(xli) && a1 < 0) ad = fmin(ad, qd(-tau * S.zl[i], a1));
+        if (S.hasu(xui) && a2 < 0) ad = fmin(ad, qd(-tau * S.zu[i], a2));
       });
       ftb_p = wmin(ap);
       ftb_d = wmin(ad);
@@ -4341,9 +4396,9 @@ __device__ __forceinline__ int solve_one(Solver<CAP>& S, const Params* __restric
         S.dz_x(i, dUa[i], dzl, dzu);
         double nzl = S.zl[i] + ad * dzl, nzu = S.zu[i] + ad * dzu;
         const double un = S.Ut[i];
-        if (S.hasl(S.xl[i])) { const double Sn = un - S.xl[i]; nzl = fmax(fmin(nzl, ks * mu / Sn), mu / (ks * Sn)); }
+        if (S.hasl(S.xl[i])) { const double Sn = un - S.xl[i]; nzl = fmax(fmin(nzl, qd(ks * mu, Sn)), qd(mu, ks * Sn)); }
         else nzl = 0.0;
-        if (S.hasu(S.xu[i])) { const double Sn = S.xu[i] - un; nzu = fmax(fmin(nzu, ks * mu / Sn), mu / (ks * Sn)); }
+        if (S.hasu(S.xu[i])) { const double Sn = S.xu[i] - un; nzu = fmax(fmin(nzu, qd(ks * mu, Sn)), qd(mu, ks * Sn)); }
         else nzu = 0.0;
         if (on) { S.zl[i] = nzl; S.zu[i] = nzu; S.U[i] = un; }
       });
@@ -4361,9 +4416,9 @@ __device__ __forceinline__ int solve_one(Solver<CAP>& S, const Params* __restric
         const double dyv = S.eqlo(lo) ? ((acc_kind == 2) ? S.eqy2_()[r] : S.eqy_()[r]) : D * dsr + rs;
         const double sn = sr + ap * dsr;
         double nvl = vlr + ad * dvl, nvu = vur + ad * dvu;
-        if (hl) { const double Sn = sn - lo; nvl = fmax(fmin(nvl, ks * mu / Sn), mu / (ks * Sn)); }
+        if (hl) { const double Sn = sn - lo; nvl = fmax(fmin(nvl, qd(ks * mu, Sn)), qd(mu, ks * Sn)); }
         else nvl = 0.0;
-        if (hu) { const double Sn = hi - sn; nvu = fmax(fmin(nvu, ks * mu / Sn), mu / (ks * Sn)); }
+        if (hu) { const double Sn = hi - sn; nvu = fmax(fmin(nvu, qd(ks * mu, Sn)), qd(mu, ks * Sn)); }
         else nvu = 0.0;
         if (on) {
           S.y[r] = yr + ap * dyv;
