@@ -12,7 +12,7 @@ set -o pipefail
 TAG=${1:-r02}
 R=$PWD
 cd /tmp && export TMPDIR=/tmp
-B="$R/bench.py --no-cpu-baseline --no-per-step --warmup 5 ${BENCH_ARGS:-}"
+B="$R/bench.py --no-cpu-baseline --no-per-step --no-config5 --warmup 5 ${BENCH_ARGS:-}"
 O=$R/gpurun_out
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_${TAG}_stats -o run -- python3 $B > $O/prof_${TAG}_stats.log 2>&1
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d $O/prof_${TAG}_fetch -o run -- python3 $B > $O/prof_${TAG}_fetch.log 2>&1
