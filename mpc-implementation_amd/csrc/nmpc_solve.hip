@@ -1049,6 +1049,15 @@ struct Solver {
     E23 = T * v * ct;
     b00 = T * cp * ct; b10 = T * sp * ct; b20 = T * stt;
   }
+  // a stage's A / B entries, formed a stage ahead in the backward sweeps: they depend on
+  // trig only, not on the recursion, and formed at the stage itself their LDS reads and
+  // three-deep products sat on the stage's critical path behind its barrier
+  struct StageAB { double E03, E04, E13, E14, E23, b00, b10, b20; };
+  __device__ __forceinline__ StageAB stage_ab(int k, double T) const {
+    StageAB a;
+    stage_AB(k, T, a.E03, a.E04, a.E13, a.E14, a.E23, a.b00, a.b10, a.b20);
+    return a;
+  }
 
   // --------------------------------------------- adjoint lam_k (lanef() = k)
   // lam_N = G_N^T y_N; lam_k = ofac*gl_k + G_k^T y_k + A_k^T lam_{k+1}
@@ -1659,6 +1668,40 @@ struct Solver {
       const LDS double* xk = X + k * 8;
       double Qxy0 = 0, Qxy1 = 0, Qxy2 = 0, qx = 0, qy = 0;
       double Qb[5] = {0, 0, 0, 0, 0}, qb[5] = {0, 0, 0, 0, 0};
+      if constexpr (CAP::deep) {
+        // the deep (LDS) class: unrolled over the class's row maximum with clamped rows, so
+        // every row's loads and its obstacle's reciprocal square root issue without waiting
+        // for the previous row (a rolled loop with the branch on the row kind left each
+        // row's rsq chain exposed); the sums take the active obstacle rows in order, as
+        // below -- the same operations in the same order
+#pragma unroll
+        for (int i = 0; i < CAP::mmax; ++i) {
+          const bool act = i < m;
+          const int ic = act ? i : m - 1;
+          const int r = k * m + ic;
+          const double w = soc ? 0.0 : Wr[r], bw = Br[r];
+          const bool box = ic < nb;
+          if (i < 5) {
+            if (act && box) {
+              Qb[i] = w;
+              qb[i] = bw;
+            }
+          }
+          const double C = curv ? y[r] * dc[r] : 0.0;
+          const int o = box ? 0 : ic - nb;
+          const double ddx = xk[0] - obx[o], ddy = xk[1] - oby[o];
+          const double idd = rsq(ddx * ddx + ddy * ddy);
+          const double gx = -(ddx * idd), gy = -(ddy * idd);
+          const double id3 = idd * idd * idd;
+          if (act && !box) {
+            Qxy0 += w * gx * gx + C * (-ddy * ddy * id3);
+            Qxy1 += w * gx * gy + C * (ddx * ddy * id3);
+            Qxy2 += w * gy * gy + C * (-ddx * ddx * id3);
+            qx += bw * gx;
+            qy += bw * gy;
+          }
+        }
+      } else
       for (int i = 0; i < m; ++i) {
         const int r = k * m + i;
         const double w = soc ? 0.0 : Wr[r], bw = Br[r];
@@ -1829,12 +1872,14 @@ struct Solver {
     sync();
     bool ok = true;
     // one stage of the backward sweep (false: a pivot is not positive)
-    auto stage = [&](int k, double qvd, double rdd, double rvd) -> bool {
+    auto stage = [&](int k, double qvd, double rdd, double rvd, const StageAB& ab, StageAB& abn) -> bool {
       const R qv = (R)qvd, rdk = (R)rdd, rvk = (R)rvd;
-      double E03d, E04d, E13d, E14d, E23d, b00d, b10d, b20d;
-      stage_AB(k, Tv, E03d, E04d, E13d, E14d, E23d, b00d, b10d, b20d);
-      const R E03 = (R)E03d, E04 = (R)E04d, E13 = (R)E13d, E14 = (R)E14d, E23 = (R)E23d;
-      const R b00 = (R)b00d, b10 = (R)b10d, b20 = (R)b20d;
+      // the deep (LDS) class forms the next stage's A / B here, off the critical path; the
+      // register-limited global-row classes form each stage's at the stage (they spill)
+      const StageAB abk = CAP::deep ? ab : stage_ab(k, Tv);
+      if constexpr (CAP::deep) abn = stage_ab(k > 0 ? k - 1 : 0, Tv);
+      const R E03 = (R)abk.E03, E04 = (R)abk.E04, E13 = (R)abk.E13, E14 = (R)abk.E14, E23 = (R)abk.E23;
+      const R b00 = (R)abk.b00, b10 = (R)abk.b10, b20 = (R)abk.b20;
       const R zr = (R)0;
       // fixed controls (make_parameter) leave the stage problem: unit pivot, no coupling;
       // the mask is wave-uniform, so its handling is a scalar branch skipped when 0
@@ -2017,17 +2062,19 @@ struct Solver {
     // two stages per trip, their prefetched operands in alternating registers: no
     // loop-carried register copies (which made the loop latch wait for every store)
     double qB, rB, vB;
+    StageAB abA, abB;
+    if constexpr (CAP::deep) abA = stage_ab(N - 1, Tv);
     for (int k = N - 1; k >= 0; k -= 2) {
       {
         const int kp = k > 0 ? k - 1 : 0;
         qB = Qsl[kp * 36]; rB = Rdl[kp * 6]; vB = rvl[kp * 6];
       }
-      if (!stage(k, qvn, rdn, rvn) || k == 0) break;
+      if (!stage(k, qvn, rdn, rvn, abA, abB) || k == 0) break;
       {
         const int kp = k > 1 ? k - 2 : 0;
         qvn = Qsl[kp * 36]; rdn = Rdl[kp * 6]; rvn = rvl[kp * 6];
       }
-      if (!stage(k - 1, qB, rB, vB)) break;
+      if (!stage(k - 1, qB, rB, vB, abB, abA)) break;
     }
     if constexpr (SG) nneg = __builtin_amdgcn_readfirstlane(negs);
     return ok;
@@ -2061,11 +2108,11 @@ struct Solver {
     const GLB double* const Kl = K + li;  // this lane's K column: K_k[r][li] = Kl[k*48 + r*8]
     sync();
     // one stage of the backward recursion with its stored r_k (rin) and K column (kc)
-    auto stage = [&](int k, const R (&rin)[6], const R (&kc)[6]) {
-      double E03d, E04d, E13d, E14d, E23d, b00d, b10d, b20d;
-      stage_AB(k, E03d, E04d, E13d, E14d, E23d, b00d, b10d, b20d);
-      const R E03 = (R)E03d, E04 = (R)E04d, E13 = (R)E13d, E14 = (R)E14d, E23 = (R)E23d;
-      const R b00 = (R)b00d, b10 = (R)b10d, b20 = (R)b20d, Tr = (R)T;
+    auto stage = [&](int k, const R (&rin)[6], const R (&kc)[6], const StageAB& ab, StageAB& abn) {
+      const StageAB abk = CAP::deep ? ab : stage_ab(k, T);  // (as in riccati_)
+      if constexpr (CAP::deep) abn = stage_ab(k > 0 ? k - 1 : 0, T);
+      const R E03 = (R)abk.E03, E04 = (R)abk.E04, E13 = (R)abk.E13, E14 = (R)abk.E14, E23 = (R)abk.E23;
+      const R b00 = (R)abk.b00, b10 = (R)abk.b10, b20 = (R)abk.b20, Tr = (R)T;
       R p8[8];
 #pragma unroll
       for (int i = 0; i < 8; ++i) p8[i] = pv[i];
@@ -2108,12 +2155,14 @@ struct Solver {
       for (int r = 0; r < 6; ++r) ko[r] = (R)Kl[kc * 48 + r * 8];
     };
     fetch(rA, kA, N - 1);
+    StageAB abA, abB;
+    if constexpr (CAP::deep) abA = stage_ab(N - 1, T);
     for (int k = N - 1; k >= 0; k -= 2) {
       fetch(rB, kB, k - 1);
-      stage(k, rA, kA);
+      stage(k, rA, kA, abA, abB);
       if (k == 0) break;
       fetch(rA, kA, k - 2);
-      stage(k - 1, rB, kB);
+      stage(k - 1, rB, kB, abB, abA);
     }
     // k_k = -R~_k^-1 r~_k, lane k: R~_k's Cholesky factor and the two triangular solves
     if (ln < N) {
