@@ -1,6 +1,7 @@
 # round-6 final measurement, in two gpurun calls (each under the 20-minute call limit):
 #   part a: -m gpu suite, smoke, the default bench line, the config-3 rocprofv3 passes
 #   part b: the config-5 rocprofv3 passes, the step-time diagnostic, the phase builds' profiles
+#   part c5: the config-5 rocprofv3 passes alone
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 O=gpurun_out; TAG=${2:-r06}
@@ -13,6 +14,9 @@ if [ "$1" == "a" ]; then
   echo bench done
   bash scripts/profile_round.sh $TAG || exit 1
   echo "part a done tests_rc=$rc"
+elif [ "$1" == "c5" ]; then
+  BENCH_ARGS="--config 5 --batch 8192" bash scripts/profile_round.sh ${TAG}_cfg5 || exit 1
+  echo "part c5 done"
 else
   BENCH_ARGS="--config 5 --batch 8192" bash scripts/profile_round.sh ${TAG}_cfg5 || exit 1
   timeout -k 10 200 python -u scripts/step_times.py $O/${TAG}_step_times.npz > $O/${TAG}_step_times.txt 2>&1 || exit 1
