@@ -754,14 +754,16 @@ struct Solver {
   }
 
   // f = sum_k l_k(X) and rows dst[r] = dc[r] * g_r(X) (dc may be null -> unscaled)
+  // (obj = false: the rows only, f = 0 -- the restoration line search, whose trials are judged
+  // without the original objective; eval_f forms it for the accepted trial alone)
   template <class DP>
-  __device__ __forceinline__ double eval_fg(const LDS double* Xs, DP dst, const RV* scale) {
+  __device__ __forceinline__ double eval_fg(const LDS double* Xs, DP dst, const RV* scale, bool obj = true) {
     STAMP0();
     const int k = lanef();
     double f = 0.0;
     if (k <= N) {
       const LDS double* xk = Xs + k * 8;
-      if (k < N) f = stage_cost(xk, tc + k * 12);
+      if (obj && k < N) f = stage_cost(xk, tc + k * 12);
       if constexpr (!CAP::deep) {  // register-limited classes: one row at a time (fewer live values)
 #pragma unroll
         for (int i = 0; i < CAP::mmax; ++i) {
@@ -796,6 +798,20 @@ struct Solver {
       }
     }
     sync();
+    const double fs = wsum(f);
+    STAMP1(PH_EVAL);
+    return fs;
+  }
+
+  // the objective alone, sum_k l_k(X), its transcendental values into the cache buffer tcb:
+  // the same stage costs as eval_fg's, summed by the same wave reduction over the same lanes
+  // (stage k on lane k, zeros elsewhere), so the same f -- also for a pair's second trial,
+  // whose eval_fg2 sum over lanes 32 + k the butterfly forms in the same order
+  __device__ __forceinline__ double eval_f(const LDS double* Xs, GLB double* tcb) {
+    STAMP0();
+    const int k = lanef();
+    double f = 0.0;
+    if (k < N) f = stage_cost(Xs + k * 8, tcb + k * 12);
     const double fs = wsum(f);
     STAMP1(PH_EVAL);
     return fs;
@@ -884,14 +900,14 @@ struct Solver {
     sync();
   }
   // f and scaled rows of both trials (eval_fg's deep form): group 0 -> dt, f0; group 1 -> dms, f1
-  __device__ __forceinline__ void eval_fg2(double& f0, double& f1) {
+  __device__ __forceinline__ void eval_fg2(double& f0, double& f1, bool obj = true) {
     STAMP0();
     const int l = lanef();
     const int grp = l >> 5, k = l & 31;
     double f = 0.0;
     if (k <= N) {
       const LDS double* xk = (grp ? lam : Xt) + k * 8;
-      if (k < N) f = stage_cost(xk, tc + (grp ? TCS : 0) + k * 12);
+      if (obj && k < N) f = stage_cost(xk, tc + (grp ? TCS : 0) + k * 12);
       const double x0 = xk[0], x1 = xk[1];
       double gv[CAP::mmax];
 #pragma unroll
@@ -2568,10 +2584,12 @@ struct Solver {
     rvars[34] = pn; rvars[35] = lg; rvars[36] = prox;
     return pn_of(pn, lg, prox);
   }
-  // restoration trial point: theta_R, phi_R and the original objective fo
+  // restoration trial point: theta_R and phi_R (fo, fo2: 0 -- phi_R does not contain the
+  // original objective, so the trials are formed without it and the restoration phase
+  // forms it for the accepted trial alone, Solver::eval_f)
   // spec (kSpec classes): 0 this trial alone; 1 this trial and the next backtracking one
-  // (a2) formed together (rollout2 / eval_fg2; the second's objective into fo2); 2 this trial
-  // was formed as the second of a pair: its X in `lam`, its rows in `dms`, fo = fo2
+  // (a2) formed together (rollout2 / eval_fg2); 2 this trial was formed as the second of a
+  // pair: its X in `lam`, its rows in `dms`
   __device__ __forceinline__ bool trial_resto(double a, const GLB double* dUs, const RV* dss,
                                               const GLB double* dps, const GLB double* dns, double& fo,
                                               double& phit, double& tht, int spec = 0, double a2 = 0.0,
@@ -2614,7 +2632,7 @@ struct Solver {
     bool done = false;
     if constexpr (kSpec) {
       if (spec == 2) {
-        fo = *fo2;
+        fo = 0.0;
         XSTAMP0(_x3);
         rowpass(dms);
         XSTAMP1(_x3, X_TROWS);
@@ -2625,9 +2643,9 @@ struct Solver {
         XSTAMP1(_x1, X_TROLL);
         XSTAMP0(_x2);
         double f0, f1;
-        eval_fg2(f0, f1);
-        fo = df * f0;
-        *fo2 = df * f1;
+        eval_fg2(f0, f1, false);
+        fo = 0.0;
+        *fo2 = 0.0;
         XSTAMP1(_x2, X_TEVAL);
         XSTAMP0(_x3);
         rowpass(dt);
@@ -2640,7 +2658,8 @@ struct Solver {
       rollout(U, Xt, dUs, a, &up);
       XSTAMP1(_x1, X_TROLL);
       XSTAMP0(_x2);
-      fo = df * eval_fg(Xt, dt, dc);
+      fo = 0.0;
+      eval_fg(Xt, dt, dc, false);
       XSTAMP1(_x2, X_TEVAL);
       XSTAMP0(_x3);
       rowpass(dt);
@@ -3417,6 +3436,10 @@ __device__ __forceinline__ void resto_phase(const Params* __restrict__ prm, doub
         STAMPV1(_tls, PH_INIT);
         XSTAMP1(_xls, X_LS);
         if (acc == 0) { rstat = ST_RESTO_FAIL; break; }  // no restoration inside the restoration phase
+        // the accepted trial's original objective (the line search judged its trials by phi_R,
+        // which does not contain it): its X is in Xt on every path, its transcendental values
+        // go to its cache buffer, where the rollout put its cos / sin
+        V[20] = S.df * S.eval_f(S.Xt, S.tc + tcb_acc * Solver<CAP>::TCS);
         rwd_cnt = (nsteps == 0) ? 0 : rwd_cnt + 1;
         // filter augmentation (F-type + Armijo steps do not augment)
         {
